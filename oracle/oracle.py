@@ -1,0 +1,152 @@
+"""ctypes wrapper over oracle/liboracle.so -- TEST INFRASTRUCTURE ONLY.
+
+The plain-C restatement of replicat's chunker (oracle/gclmul_oracle.c, citing
+/root/reference/src/adapters.cpp:18-77 and replicat/utils/adapters.py:274-305).  Imported only
+by tests/, ``__graft_entry__.smoke()`` and bench.py's ``cpu_baseline`` leg, always as the
+checker or the reported CPU baseline -- never by ``replicat_amd`` (the product path).
+Pinned against the reference by tests/test_oracle.py (tests/golden/*.json).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, 'liboracle.so')
+
+_u64 = ctypes.c_uint64
+_p = ctypes.c_void_p
+_lib = None
+
+ERRORS = {
+    1: 'key must contain exactly 16 characters',
+    2: 'Minimum length is greater than the maximum one',
+    3: 'Bad key contents',
+}
+
+
+def build():
+    subprocess.run(['make', '-s', '-C', HERE, 'liboracle.so'], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        L.oc_key.restype = _u64
+        L.oc_key.argtypes = [_u64, _u64, _u64]
+        L.oc_key_soft.restype = _u64
+        L.oc_key_soft.argtypes = [_u64, _u64, _u64]
+        L.oc_parse_params.restype = ctypes.c_int
+        L.oc_parse_params.argtypes = [_u64, _u64, ctypes.c_char_p, _u64, _p, _p]
+        L.oc_next_cut.restype = _u64
+        L.oc_next_cut.argtypes = [_u64, _u64, _u64, _u64, _p, _u64, ctypes.c_int]
+        L.oc_chunk_stream.restype = ctypes.c_int64
+        L.oc_chunk_stream.argtypes = [_u64, _u64, _u64, _u64, _p, _u64, _u64, _p, _u64]
+        L.oc_keys_needed.restype = _u64
+        L.oc_keys_needed.argtypes = [_u64, _u64, _u64]
+        L.oc_tile_records.restype = None
+        L.oc_tile_records.argtypes = [_u64, _u64, _p, _u64, _u64, _u64, _p, _p]
+        L.oc_chunk_streams_mt.restype = ctypes.c_int
+        L.oc_chunk_streams_mt.argtypes = [_u64, _u64, _u64, _u64, _u64, _p, _p, _p, _p, _p,
+                                          _p, _p, ctypes.c_int]
+        L.oc_fill_splitmix.restype = None
+        L.oc_fill_splitmix.argtypes = [_p, _u64, _u64, _u64]
+        _lib = L
+    return _lib
+
+
+def normalize_params(params):
+    """adapters.py:280-285 (S5)."""
+    if not params:
+        return b'\xff' * 16
+    params = bytes(params)
+    while len(params) < 16:
+        params += params
+    return params[:16]
+
+
+def parse_key(min_length, max_length, key16):
+    k0, k1 = _u64(), _u64()
+    rc = lib().oc_parse_params(min_length, max_length, bytes(key16), len(key16),
+                               ctypes.byref(k0), ctypes.byref(k1))
+    if rc:
+        raise ValueError(ERRORS[rc])
+    return k0.value, k1.value
+
+
+def _buf(data):
+    arr = np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+    # the restatement may read up to 8 bytes past a 4-aligned key offset: pad a private copy
+    pad = np.zeros(len(arr) + 16, dtype=np.uint8)
+    pad[:len(arr)] = arr
+    return pad
+
+
+def chunk_stream(data, min_length, max_length, params=None, last_piece_start=0):
+    """Cut END offsets of one stream (S4 closed form over (L, P))."""
+    k0, k1 = parse_key(min_length, max_length, normalize_params(params))
+    buf = _buf(data)
+    L = len(buf) - 16
+    cap = L // 4 + 8
+    cuts = np.zeros(cap, dtype=np.uint64)
+    n = lib().oc_chunk_stream(min_length, max_length, k0, k1, buf.ctypes.data, L,
+                              last_piece_start, cuts.ctypes.data, cap)
+    assert n >= 0
+    return cuts[:n].tolist()
+
+
+def chunk_pieces(pieces, min_length, max_length, params=None):
+    """Chunk lengths the reference adapter yields for this piece list."""
+    pieces = [bytes(p) for p in pieces]
+    if not pieces:
+        return []
+    data = b''.join(pieces)
+    P = len(data) - len(pieces[-1])
+    ends = chunk_stream(data, min_length, max_length, params, P)
+    return [e - s for s, e in zip([0] + ends[:-1], ends)]
+
+
+def next_cut(data, final, min_length, max_length, params=None):
+    k0, k1 = parse_key(min_length, max_length, normalize_params(params))
+    buf = _buf(data)
+    return lib().oc_next_cut(min_length, max_length, k0, k1, buf.ctypes.data, len(buf) - 16,
+                             int(bool(final)))
+
+
+def key(k0, k1, d):
+    return lib().oc_key(k0, k1, d)
+
+
+def key_soft(k0, k1, d):
+    return lib().oc_key_soft(k0, k1, d)
+
+
+def keys_needed(max_length, L, P):
+    return lib().oc_keys_needed(max_length, L, P)
+
+
+def fill_splitmix(nbytes, seed, stream):
+    out = np.zeros(nbytes, dtype=np.uint8)
+    lib().oc_fill_splitmix(out.ctypes.data, nbytes, seed, stream)
+    return out
+
+
+def chunk_streams_mt(bufs, lens, pstarts, min_length, max_length, params=None, threads=1):
+    """Threaded CPU baseline over many host streams (each buffer padded by >= 8 bytes)."""
+    k0, k1 = parse_key(min_length, max_length, normalize_params(params))
+    n = len(bufs)
+    ptrs = np.array([b.ctypes.data for b in bufs], dtype=np.uint64)
+    L = np.asarray(lens, dtype=np.uint64)
+    P = np.asarray(pstarts, dtype=np.uint64)
+    cap = L // np.uint64(max(4, (min_length + 3) & ~3)) + np.uint64(8)
+    base = np.concatenate([[0], np.cumsum(cap)[:-1]]).astype(np.uint64)
+    cuts = np.zeros(int(cap.sum()), dtype=np.uint64)
+    counts = np.zeros(n, dtype=np.int64)
+    lib().oc_chunk_streams_mt(min_length, max_length, k0, k1, n, ptrs.ctypes.data,
+                              L.ctypes.data, P.ctypes.data, base.ctypes.data, cap.ctypes.data,
+                              cuts.ctypes.data, counts.ctypes.data, threads)
+    return [cuts[int(b):int(b) + int(c)].tolist() for b, c in zip(base, counts)]

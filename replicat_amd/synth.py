@@ -1,0 +1,45 @@
+"""Synthetic stream bytes shared by the tests, the golden-fixture script and bench.py.
+
+Stream ``s`` of a workload with seed ``seed`` is the little-endian concatenation of the
+64-bit words ``sm64(base ^ i)``, ``i = 0, 1, ...``, where ``base = (seed * GOLDEN) ^ (s << 34)``
+and ``sm64`` is the splitmix64 finaliser.  The device generator in
+``replicat_amd/csrc/chunker.hip`` (``rc_fill_splitmix``) and ``oracle/gclmul_oracle.c``
+(``oc_fill_splitmix``) write exactly the same bytes, so a multi-GiB stream never needs
+to cross PCIe to be checked.  ("splitmix64 counter stream (seed 0x5eed,
+stream id in high bits)".)
+"""
+import numpy as np
+
+GOLDEN = 0x9E3779B97F4A7C15
+M64 = (1 << 64) - 1
+DEFAULT_SEED = 0x5EED
+
+
+def stream_base(seed: int, stream: int) -> int:
+    return ((seed * GOLDEN) & M64) ^ ((stream << 34) & M64)
+
+
+def splitmix_words(base: int, start: int, count: int) -> np.ndarray:
+    """Words ``start .. start+count-1`` of the counter stream with the given base."""
+    with np.errstate(over='ignore'):
+        z = np.arange(start, start + count, dtype=np.uint64)
+        z ^= np.uint64(base)
+        z += np.uint64(GOLDEN)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z ^= z >> np.uint64(31)
+    return z
+
+
+def stream_bytes(nbytes: int, seed: int = DEFAULT_SEED, stream: int = 0) -> np.ndarray:
+    """``nbytes`` bytes of synthetic stream ``stream`` as a uint8 array."""
+    words = splitmix_words(stream_base(seed, stream), 0, (nbytes + 7) // 8)
+    return words.view('<u1')[:nbytes].copy() if nbytes % 8 else words.view('<u1')
+
+
+def seeded_key(seed: int) -> bytes:
+    """A 16-byte chunker key (k0 != 0) derived from ``seed`` -- the 'generic key' leg."""
+    w = splitmix_words(stream_base(seed, 0x3FFF), 0, 2)
+    if int(w[0]) == 0:
+        w[0] = np.uint64(1)
+    return w.astype('<u8').tobytes()

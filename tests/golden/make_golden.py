@@ -1,0 +1,258 @@
+"""Generate tests/golden/*.json from the REFERENCE chunker (build container only).
+
+Runs replicat's own adapter (``replicat.utils.adapters.gclmulchunker``, imported from
+/root/reference) over its own ``_replicat_adapters`` extension, compiled from
+/root/reference/src/adapters.cpp by ``make -C oracle ref`` into oracle/_ref/.  Neither travels
+to the GPU box: only the JSON this script writes does.
+
+    make -C oracle ref
+    PYTHONPATH=oracle/_ref:/root/reference PYTHONDONTWRITEBYTECODE=1 \
+        python tests/golden/make_golden.py
+
+Inputs are reproducible without the reference: CPython ``random.Random(seed).randbytes`` for
+small cases (what the reference's own tests use, replicat/utils/compat.py:5-12) and the
+splitmix64 counter streams of ``replicat_amd.synth`` for large ones.
+"""
+import hashlib
+import json
+import multiprocessing as mp
+import os
+import random
+import struct
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+
+from replicat.utils import adapters  # noqa: E402  (reference)
+from replicat_amd import synth  # noqa: E402
+
+MIN_DEF, MAX_DEF = 128_000, 5_120_000
+
+
+def ref_lengths(min_length, max_length, pieces, params):
+    chunker = adapters.gclmulchunker(min_length=min_length, max_length=max_length)
+    return [len(c) for c in chunker(pieces, params=params)]
+
+
+# ---------------------------------------------------------------- small cases
+
+
+def small_data(spec, n):
+    kind = spec[0]
+    if kind == 'mt':
+        return random.Random(spec[1]).randbytes(n)
+    if kind == 'zero':
+        return bytes(n)
+    if kind == 'const':
+        return bytes([spec[1]]) * n
+    if kind == 'repeat':
+        unit = random.Random(spec[1]).randbytes(spec[2])
+        return (unit * (n // len(unit) + 1))[:n]
+    raise ValueError(spec)
+
+
+def split_pieces(data, cuts):
+    out, prev = [], 0
+    for c in cuts + [len(data)]:
+        out.append(data[prev:c])
+        prev = c
+    return out
+
+
+def make_small_cases(count=320, seed=20261015):
+    rnd = random.Random(seed)
+    cases = []
+    for n in range(count):
+        aligned = n % 4 != 3  # 3 in 4 cases inside the multi-piece parity domain
+        max_length = rnd.choice([4, 8, 12, 64, 100, 256, 1000, 4096, 10_000, 20_000])
+        if aligned:
+            max_length = max(4, max_length - max_length % 4)
+        else:
+            max_length += rnd.randrange(1, 4)
+        min_length = rnd.randrange(1, max_length + 1)
+        if rnd.random() < 0.15:
+            min_length = max_length
+        total = rnd.choice([0, 1, 3, 7, max_length - 1, max_length, 2 * max_length - 1,
+                            2 * max_length, rnd.randrange(0, 64 * max_length + 1)])
+        total = max(0, min(total, 200_000))
+        dkind = rnd.random()
+        if dkind < 0.75:
+            spec = ['mt', rnd.randrange(1 << 30)]
+        elif dkind < 0.83:
+            spec = ['zero']
+        elif dkind < 0.90:
+            spec = ['const', rnd.randrange(256)]
+        else:
+            spec = ['repeat', rnd.randrange(1 << 30), rnd.randrange(1, 5000)]
+        data = small_data(spec, total)
+        if aligned and total and rnd.random() < 0.6:
+            k = rnd.randrange(1, 12)
+            cuts = sorted(rnd.randrange(0, total + 1) for _ in range(k))
+        elif aligned and 0 < total <= 64 and rnd.random() < 0.5:
+            cuts = list(range(1, total))  # one byte per piece (cf. test_adapters.py:287-289)
+        else:
+            cuts = []
+        pieces = split_pieces(data, cuts)
+        pk = rnd.random()
+        if pk < 0.3:
+            params = None
+        elif pk < 0.85:
+            params = rnd.randbytes(16)
+            if params[:8] == bytes(8):
+                params = b'\x01' + params[1:]
+        else:
+            params = rnd.randbytes(rnd.randrange(1, 16))
+            if params[0] == 0:
+                params = b'\x02' + params[1:]
+        cases.append({
+            'min': min_length, 'max': max_length, 'data': spec, 'size': total,
+            'pieces': [len(p) for p in pieces],
+            'params': None if params is None else params.hex(),
+            'expected': ref_lengths(min_length, max_length, pieces, params),
+        })
+    return cases
+
+
+def make_known_answers():
+    """The reference's own test inputs (replicat/tests/test_adapters.py:273-364), as data."""
+    out = {'alignment': [], 'seeded': []}
+    for (mn, mx, piece, npieces, total) in [
+        (5, 10, 0, 0, 0), (5, 10, 5, 1, 5), (5, 10, 6, 1, 6), (5, 10, 10, 1, 10),
+        (5, 10, 11, 1, 11), (5, 10, 12, 1, 12), (5, 10, 13, 1, 13), (5, 10, 14, 1, 14),
+        (5, 10, 15, 1, 15), (5, 10, 16, 1, 16), (5, 10, 17, 1, 17), (5, 10, 18, 1, 18),
+        (5, 10, 19, 1, 19), (4, 4, 1, 20, 20), (4, 4, 20, 1, 20), (10, 12, 1, 11, 11),
+    ]:
+        pieces = [b'\xaa' * piece] * npieces
+        out['alignment'].append({'min': mn, 'max': mx, 'byte': 0xAA, 'pieces': [piece] * npieces,
+                                 'expected': ref_lengths(mn, mx, pieces, None)})
+    # personalization (:301-313), sequence_stabilizes (:315-336), repetition (:338-364)
+    rnd = random.Random(0)
+    data = rnd.randbytes(1_000_000)
+    person = bytearray(rnd.randbytes(16))
+    out['seeded'].append({'name': 'personalization', 'seed': 0, 'size': 1_000_000, 'repeat': 1,
+                          'params': bytes(person).hex(),
+                          'expected': ref_lengths(500, 10_000, [data], bytes(person))})
+    person[0] = (person[0] - 1) % 255
+    out['seeded'].append({'name': 'personalization_flipped', 'seed': 0, 'size': 1_000_000,
+                          'repeat': 1, 'params': bytes(person).hex(),
+                          'expected': ref_lengths(500, 10_000, [data], bytes(person))})
+    for seed in (507, 11219, 25750, 31286):
+        rnd = random.Random(seed)
+        data = bytearray(rnd.randbytes(1_000_000))
+        person = rnd.randbytes(16)
+        before = ref_lengths(500, 10_000, [bytes(data)], person)
+        data[0] = (data[0] - 1) % 255
+        after = ref_lengths(500, 10_000, [bytes(data)], person)
+        out['seeded'].append({'name': 'stabilizes', 'seed': seed, 'size': 1_000_000,
+                              'repeat': 1, 'params': person.hex(), 'expected': before,
+                              'expected_after_flip0': after})
+    for seed, size in [(0, 1_001), (1, 2_000), (2, 497), (2, 4_023), (3, 5_001)]:
+        rnd = random.Random(seed)
+        unit = rnd.randbytes(size)
+        person = rnd.randbytes(16)
+        for reps in (50, 100):
+            out['seeded'].append({'name': 'repetition', 'seed': seed, 'size': size,
+                                  'repeat': reps, 'params': person.hex(),
+                                  'expected': ref_lengths(500, 10_000, [unit] * reps, person)})
+    return out
+
+
+# ------------------------------------------------------------- large streams
+
+
+def _stream_job(job):
+    kind, args = job
+    if kind == 'splitmix':
+        seed, idx, nbytes, piece, mn, mx, key = args
+        data = synth.stream_bytes(nbytes, seed, idx).tobytes()
+    elif kind == 'fill':
+        value, nbytes, piece, mn, mx, key = args
+        data = bytes([value]) * nbytes
+    else:
+        raise ValueError(kind)
+    if piece:
+        pieces = [data[i:i + piece] for i in range(0, len(data), piece)]
+    else:
+        pieces = [data]
+    lens = ref_lengths(mn, mx, pieces, None if key is None else bytes.fromhex(key))
+    ends, acc = [], 0
+    for x in lens:
+        acc += x
+        ends.append(acc)
+    return ends
+
+
+def cutlist_digest(all_ends):
+    h = hashlib.sha256()
+    for ends in all_ends:
+        h.update(struct.pack('<Q', len(ends)))
+        h.update(struct.pack('<%dQ' % len(ends), *ends))
+    return h.hexdigest()
+
+
+def make_streams(pool):
+    seeded = synth.seeded_key(1).hex()
+    specs = []
+    for key in (None, seeded):
+        for i in range(4):
+            specs.append(('splitmix', (synth.DEFAULT_SEED, i, 64 << 20, 0, MIN_DEF, MAX_DEF, key)))
+    specs.append(('splitmix', (synth.DEFAULT_SEED, 7, 256 << 20, 16 << 20, MIN_DEF, MAX_DEF, None)))
+    specs.append(('splitmix', (synth.DEFAULT_SEED, 8, (48 << 20) + 12345, 0, MIN_DEF, MAX_DEF, seeded)))
+    specs.append(('fill', (0, 16 << 20, 0, MIN_DEF, MAX_DEF, None)))
+    specs.append(('fill', (0xAA, 16 << 20, 0, MIN_DEF, MAX_DEF, seeded)))
+    for i in range(4):
+        specs.append(('splitmix', (synth.DEFAULT_SEED, i, 1 << 20, 0, MIN_DEF, MAX_DEF, None)))
+        specs.append(('splitmix', (synth.DEFAULT_SEED, i, 1 << 20, 0, 2_000, 80_000, None)))
+    results = pool.map(_stream_job, specs)
+    out = []
+    for (kind, args), ends in zip(specs, results):
+        if kind == 'splitmix':
+            seed, idx, nbytes, piece, mn, mx, key = args
+            d = {'data': ['splitmix', seed, idx], 'size': nbytes}
+        else:
+            value, nbytes, piece, mn, mx, key = args
+            d = {'data': ['fill', value], 'size': nbytes}
+        d.update({'piece': piece, 'min': mn, 'max': mx, 'params': key, 'ends': ends})
+        out.append(d)
+    return out
+
+
+def make_digests(pool, quick=False):
+    seeded = synth.seeded_key(1).hex()
+    sets = [
+        # config 2: 1024 x 64 MiB, default params, unencrypted key (0xff * 16)
+        ('config2_ff', 1024, 64 << 20, MIN_DEF, MAX_DEF, None),
+        # config 2 subset with a generic key
+        ('config2_seeded_first128', 128, 64 << 20, MIN_DEF, MAX_DEF, seeded),
+        # config 3 (iii): non-default params on 1 MiB streams (first 4096 of 65536)
+        ('config3iii_first4096', 4096, 1 << 20, 2_000, 80_000, None),
+    ]
+    out = []
+    for name, n, size, mn, mx, key in sets:
+        if quick:
+            n = min(n, 16)
+        jobs = [('splitmix', (synth.DEFAULT_SEED, i, size, 0, mn, mx, key)) for i in range(n)]
+        ends = pool.map(_stream_job, jobs, chunksize=4)
+        out.append({'name': name, 'streams': n, 'size': size, 'seed': synth.DEFAULT_SEED,
+                    'min': mn, 'max': mx, 'params': key, 'chunks': sum(map(len, ends)),
+                    'sha256': cutlist_digest(ends)})
+        print(name, out[-1]['chunks'], out[-1]['sha256'], flush=True)
+    return out
+
+
+def main():
+    quick = '--quick' in sys.argv
+    def dump(name, obj):
+        with open(os.path.join(HERE, name), 'w') as f:
+            json.dump(obj, f, separators=(',', ':'))
+            f.write('\n')
+    dump('small_cases.json', make_small_cases())
+    dump('known_answers.json', make_known_answers())
+    with mp.get_context('fork').Pool(8) as pool:
+        dump('streams.json', make_streams(pool))
+        dump('digests.json', make_digests(pool, quick))
+
+
+if __name__ == '__main__':
+    main()
