@@ -1,0 +1,128 @@
+/*
+ * replicat_chunker.h -- C ABI of the MI355X (gfx950) content-defined chunker.
+ *
+ * Drop-in boundary for replicat's native chunker module `_replicat_adapters`
+ * (/root/reference/src/adapters.cpp:80-86, stub stubs/_replicat_adapters.pyi:3-8).
+ * Plain pointers and sizes only; no torch types.  Implemented by
+ * replicat_amd/csrc/{capi.cpp,kernels.hip} -> replicat_amd/libreplicat_chunker.so.
+ *
+ * The chunk rule reproduced bit for bit:
+ *   key(p)   = k1 ^ lo(k0 (x) d) ^ lo(0x1B (x) hi(k0 (x) d)),  d = LE64(buf[p-4 .. p+4])
+ *              (x) = carry-less multiply          -- adapters.cpp:72-77
+ *   next_cut = first argmax of key over p = 4, 8, .. < max_length, forced up to
+ *              roundup4(min_length); tail rules for a final buffer < 2*max_length
+ *                                                  -- adapters.cpp:42-70
+ *   framing  = a stream of L bytes whose last piece starts at byte P is chunked exactly as
+ *              replicat's Python adapter loop chunks its pieces  -- adapters.py:290-305
+ *
+ * Error codes: RC_OK, or one of the reference constructor's three ValueErrors
+ * (adapters.cpp:21-29, same check order), or an RC_ERR_* of this library.
+ * rc_last_error() returns the message of the calling thread's last failure.
+ */
+#ifndef REPLICAT_CHUNKER_H
+#define REPLICAT_CHUNKER_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RC_OK 0
+#define RC_ERR_KEY_LENGTH 1 /* "key must contain exactly 16 characters"          adapters.cpp:21-22 */
+#define RC_ERR_MIN_GT_MAX 2 /* "Minimum length is greater than the maximum one"  adapters.cpp:23-24 */
+#define RC_ERR_BAD_KEY 3    /* "Bad key contents" (k0 == 0)                      adapters.cpp:28-29 */
+#define RC_ERR_ARGUMENT 10  /* bad pointer / size / P > L                                       */
+#define RC_ERR_ALIGN 11     /* a device stream base is not 16-byte aligned                      */
+#define RC_ERR_HIP 12       /* a HIP runtime call failed (message in rc_last_error)             */
+#define RC_ERR_OVERFLOW 13  /* a stream produced more cuts than its capacity (never expected)   */
+#define RC_ERR_NO_DEVICE 14 /* no usable gfx950 device                                          */
+
+/* rc_chunk_* flags */
+#define RC_OPEN 1u /* every stream is an OPEN prefix: its bytes all belong to non-final pieces, so
+                      the chain cuts only while L - s >= max_length and never applies the tail
+                      rule (the adapter's non-final next_cut calls, adapters.py:295-301); the
+                      uncut remainder starts at the last reported cut (0 if none).  last_piece is
+                      ignored. */
+
+typedef struct rc_chunker rc_chunker;
+
+/* Library / ABI version, e.g. 100 = 0.1.0. */
+int rc_version(void);
+
+/* Message of this thread's last error ("" if none). */
+const char *rc_last_error(void);
+
+/* Constructor of `_gclmulchunker(min_length, max_length, key)` (adapters.cpp:18-34):
+ * validates key_len == 16, min <= max, k0 != 0 in that order, then builds the GF(2) lookup
+ * tables of the key and uploads them to `device` (a HIP device ordinal).  On success *out owns
+ * device memory until rc_chunker_destroy. */
+int rc_chunker_create(uint64_t min_length, uint64_t max_length, const uint8_t *key,
+                      uint64_t key_len, int device, rc_chunker **out);
+void rc_chunker_destroy(rc_chunker *ch);
+
+/* The readonly `min_length` / `max_length` attributes (adapters.cpp:83-84). */
+uint64_t rc_chunker_min_length(const rc_chunker *ch);
+uint64_t rc_chunker_max_length(const rc_chunker *ch);
+
+/* `next_cut(buffer, final)` (adapters.cpp:42-70) on a HOST buffer: returns the cut length
+ * in *out_cut (0 = "need more data").  Tail and wait decisions are taken on the host; an
+ * argmax copies the first <= max_length+3 bytes to the device, runs the device kernels and
+ * waits for the answer.  Blocking. */
+int rc_next_cut(rc_chunker *ch, const uint8_t *buffer, uint64_t size, int final,
+                uint64_t *out_cut);
+
+/* Capacity (in cuts) that stream i of length lens[i] needs: caps[i] = L / max(4, roundup4(min))
+ * + 3.  Returns the sum over all n streams (the size of the `cuts` array below). */
+uint64_t rc_cut_capacity(const rc_chunker *ch, uint64_t n, const uint64_t *lens,
+                         uint64_t *caps /* may be NULL */);
+
+/* Batch entry point over DEVICE-resident streams (the batching shim of SURVEY.md §8 b):
+ *   d_streams[i]  device pointer to stream i (16-byte aligned), lens[i] = L_i bytes,
+ *   last_piece[i] = P_i, start of the stream's last piece (0 = one piece; P_i <= L_i).
+ * Writes stream i's chunk END offsets (u64, relative to the stream) to
+ * d_cuts[cut_base[i] ..] where cut_base = exclusive prefix sum of the capacities of
+ * rc_cut_capacity, and the count to d_counts[i] (int64; -1 = capacity overflow).
+ * The host arrays are read before return; the work is enqueued on `hip_stream` (a
+ * hipStream_t, NULL = default stream) and the call returns without synchronising. */
+int rc_chunk_device(rc_chunker *ch, uint64_t n, const uint8_t *const *d_streams,
+                    const uint64_t *lens, const uint64_t *last_piece, uint32_t flags,
+                    uint64_t *d_cuts, int64_t *d_counts, void *hip_stream);
+
+/* The same over HOST-resident streams, blocking: pinned double-buffered H2D copies overlap
+ * the kernels of the previous batch; cuts come back to host arrays laid out as above
+ * (cuts[cut_base[i] ..], counts[i]).  This is the end-to-end path of DESIGN.md. */
+int rc_chunk_host(rc_chunker *ch, uint64_t n, const uint8_t *const *streams,
+                  const uint64_t *lens, const uint64_t *last_piece, uint32_t flags,
+                  uint64_t *cuts, int64_t *counts);
+
+/* Kernel timing, for bench.py's roofline: while enabled, every rc_chunk_device call records
+ * HIP events around its tile kernel (phase A) and its chain kernel (phase B) on the launch
+ * stream.  rc_timing_read waits for the recorded events, returns the summed milliseconds and
+ * the number of calls, and clears the record. */
+int rc_timing_enable(rc_chunker *ch, int enable);
+int rc_timing_read(rc_chunker *ch, double *phase_a_ms, double *phase_b_ms, uint64_t *calls);
+
+/* Synthetic stream bytes on the device (replicat_amd/synth.py): word i of stream `stream`
+ * is splitmix64((seed * 0x9E3779B97F4A7C15) ^ (stream << 34) ^ i), little-endian. */
+int rc_fill_splitmix(uint8_t *d_dst, uint64_t nbytes, uint64_t seed, uint64_t stream,
+                     void *hip_stream);
+
+/* Keys j (key j covers bytes [4j-4, 4j+4)) that any argmax window of a stream (L, P) can
+ * reach: the largest such j, or 0 when the stream never hashes (tail rule only). */
+uint64_t rc_keys_needed(uint64_t max_length, uint64_t L, uint64_t P);
+
+/* One 64-bit key of the chunker on the host, from its lookup tables (tests / tooling). */
+uint64_t rc_host_key(const rc_chunker *ch, uint64_t d);
+
+/* Host-only check of the table construction (no device needed): out[i] = key of data word
+ * ds[i] under the 16-byte key, evaluated from the same byte tables the kernels use, and
+ * top16[i] = its top 16 bits as the prefilter tables give them. */
+int rc_tables_key(const uint8_t *key16, uint64_t n, const uint64_t *ds, uint64_t *out,
+                  uint32_t *top16);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* REPLICAT_CHUNKER_H */

@@ -1,0 +1,99 @@
+"""ctypes binding of the C ABI (include/replicat_chunker.h) -> libreplicat_chunker.so.
+
+There is no fallback: if the in-tree HIP library is missing or cannot be loaded, every entry
+point raises ``ChunkerUnavailable``.  Loading the library does not need a GPU; creating a
+chunker does (``RC_ERR_NO_DEVICE`` otherwise).
+"""
+import ctypes
+import os
+import threading
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, 'libreplicat_chunker.so')
+
+RC_OK = 0
+RC_ERR_KEY_LENGTH = 1
+RC_ERR_MIN_GT_MAX = 2
+RC_ERR_BAD_KEY = 3
+RC_ERR_ARGUMENT = 10
+RC_ERR_ALIGN = 11
+RC_ERR_HIP = 12
+RC_ERR_OVERFLOW = 13
+RC_ERR_NO_DEVICE = 14
+RC_OPEN = 1
+
+# every symbol include/replicat_chunker.h declares: name -> (restype, argtypes)
+_u64, _i64, _u32, _int, _p = ctypes.c_uint64, ctypes.c_int64, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p
+SIGNATURES = {
+    'rc_version': (_int, []),
+    'rc_last_error': (ctypes.c_char_p, []),
+    'rc_chunker_create': (_int, [_u64, _u64, _p, _u64, _int, ctypes.POINTER(_p)]),
+    'rc_chunker_destroy': (None, [_p]),
+    'rc_chunker_min_length': (_u64, [_p]),
+    'rc_chunker_max_length': (_u64, [_p]),
+    'rc_next_cut': (_int, [_p, _p, _u64, _int, ctypes.POINTER(_u64)]),
+    'rc_cut_capacity': (_u64, [_p, _u64, _p, _p]),
+    'rc_chunk_device': (_int, [_p, _u64, _p, _p, _p, _u32, _p, _p, _p]),
+    'rc_chunk_host': (_int, [_p, _u64, _p, _p, _p, _u32, _p, _p]),
+    'rc_timing_enable': (_int, [_p, _int]),
+    'rc_timing_read': (_int, [_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                              ctypes.POINTER(_u64)]),
+    'rc_fill_splitmix': (_int, [_p, _u64, _u64, _u64, _p]),
+    'rc_keys_needed': (_u64, [_u64, _u64, _u64]),
+    'rc_host_key': (_u64, [_p, _u64]),
+    'rc_tables_key': (_int, [_p, _u64, _p, _p, _p]),
+}
+
+
+class ChunkerUnavailable(RuntimeError):
+    """The HIP chunker library is not built or cannot run here."""
+
+
+class ChunkerError(RuntimeError):
+    def __init__(self, code, message):
+        super().__init__(f'{message} (rc={code})')
+        self.code = code
+
+
+_lock = threading.Lock()
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise ChunkerUnavailable(
+                    f'{LIB_PATH} is missing: build it with `python -m replicat_amd.build` '
+                    '(hipcc, gfx950); there is no CPU fallback')
+            try:
+                L = ctypes.CDLL(LIB_PATH)
+            except OSError as e:
+                raise ChunkerUnavailable(f'cannot load {LIB_PATH}: {e}') from e
+            for name, (res, args) in SIGNATURES.items():
+                f = getattr(L, name)
+                f.restype = res
+                f.argtypes = args
+            _lib = L
+    return _lib
+
+
+def last_error():
+    msg = lib().rc_last_error()
+    return msg.decode('utf-8', 'replace') if msg else ''
+
+
+def check(code):
+    """Raise for a non-zero status: the three constructor errors as the reference's ValueErrors
+    (src/adapters.cpp:21-29), everything else as ChunkerError/ChunkerUnavailable."""
+    if code == RC_OK:
+        return
+    msg = last_error()
+    if code in (RC_ERR_KEY_LENGTH, RC_ERR_MIN_GT_MAX, RC_ERR_BAD_KEY):
+        raise ValueError(msg)
+    if code == RC_ERR_NO_DEVICE:
+        raise ChunkerUnavailable(msg)
+    raise ChunkerError(code, msg)

@@ -1,0 +1,46 @@
+"""Build libreplicat_chunker.so in-tree: hipcc, gfx950 only, no torch extension machinery.
+
+    python -m replicat_amd.build        (also run by __graft_entry__.build())
+"""
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, 'csrc')
+LIB = os.path.join(HERE, 'libreplicat_chunker.so')
+SOURCES = [os.path.join(CSRC, 'kernels.hip'), os.path.join(CSRC, 'capi.cpp')]
+HEADERS = [os.path.join(CSRC, 'gclmul.h'), os.path.join(ROOT, 'include', 'replicat_chunker.h')]
+ARCH = 'gfx950'
+
+
+def hipcc():
+    for cand in (os.environ.get('HIPCC'), '/opt/rocm/bin/hipcc', shutil.which('hipcc')):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError('hipcc not found (ROCm 7.x required)')
+
+
+def stale():
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    return any(os.path.getmtime(p) > t for p in SOURCES + HEADERS)
+
+
+def build(force=False, verbose=False):
+    if not force and not stale():
+        return LIB
+    cmd = [hipcc(), f'--offload-arch={ARCH}', '-O3', '-std=c++17', '-fPIC', '-shared', '-Wall',
+           '-I', os.path.join(ROOT, 'include'), *SOURCES, '-o', LIB + '.tmp']
+    if verbose:
+        print(' '.join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(LIB + '.tmp', LIB)
+    return LIB
+
+
+if __name__ == '__main__':
+    build(force='--force' in sys.argv, verbose=True)

@@ -1,0 +1,149 @@
+"""Host-side API of the MI355X chunker: one ``GpuChunker`` per (key, min, max, device).
+
+Mirrors the reference's chunker object (``_replicat_adapters._gclmulchunker``,
+/root/reference/src/adapters.cpp:16-40) and adds the batch entry points of the C ABI:
+
+* ``next_cut(buffer, final)``          -- exactly adapters.cpp:42-70 on a host buffer;
+* ``chunk_device(...)``                -- many device-resident streams, results left in HBM;
+* ``chunk_host(buffers, last_piece)``  -- many host streams, pinned copies in, cuts back out.
+
+Streams follow replicat's piece framing (adapters.py:290-305): a stream of L bytes whose last
+piece starts at byte P is cut exactly as replicat's adapter loop cuts those pieces.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import RC_OPEN, check, lib
+
+MIN_LENGTH = 128_000     # replicat/utils/adapters.py:259
+MAX_LENGTH = 5_120_000   # replicat/utils/adapters.py:260
+
+
+def normalize_params(params):
+    """Chunker key from repository params: replicat/utils/adapters.py:280-285."""
+    if not params:
+        return b'\xff' * 16
+    params = bytes(params)
+    while len(params) < 16:
+        params += params
+    return params[:16]
+
+
+def _ptr_array(values):
+    return np.ascontiguousarray(np.asarray(values, dtype=np.uint64))
+
+
+class GpuChunker:
+    """A chunker bound to one HIP device (default: the current one)."""
+
+    def __init__(self, min_length, max_length, key, device=None):
+        key = bytes(key)
+        if device is None:
+            device = _current_device()
+        handle = ctypes.c_void_p()
+        check(lib().rc_chunker_create(min_length, max_length, key, len(key), int(device),
+                                      ctypes.byref(handle)))
+        self._h = handle
+        self.min_length = int(min_length)
+        self.max_length = int(max_length)
+        self.device = int(device)
+
+    def close(self):
+        h, self._h = getattr(self, '_h', None), None
+        if h:
+            lib().rc_chunker_destroy(h)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # --------------------------------------------------------------------- single buffer
+
+    def next_cut(self, data: np.ndarray, final: bool) -> int:
+        """adapters.cpp:42-70 on the bytes of a uint8 array (host memory)."""
+        out = ctypes.c_uint64()
+        check(lib().rc_next_cut(self._h, data.ctypes.data if data.size else None, data.size,
+                                1 if final else 0, ctypes.byref(out)))
+        return out.value
+
+    # ------------------------------------------------------------------------- batches
+
+    def capacity(self, lens):
+        lens = _ptr_array(lens)
+        caps = np.zeros(len(lens), dtype=np.uint64)
+        total = lib().rc_cut_capacity(self._h, len(lens), lens.ctypes.data, caps.ctypes.data)
+        return int(total), caps
+
+    def chunk_device(self, ptrs, lens, last_piece, cuts_ptr, counts_ptr, stream=0, open_=False):
+        """Enqueue the chunking of device-resident streams (raw device pointers) on a HIP
+        stream; cut END offsets land in the device array at ``cuts_ptr`` (u64, per-stream
+        regions of ``capacity(lens)`` entries) and counts at ``counts_ptr`` (int64)."""
+        ptrs, lens = _ptr_array(ptrs), _ptr_array(lens)
+        last = _ptr_array(last_piece if last_piece is not None else np.zeros(len(lens)))
+        check(lib().rc_chunk_device(self._h, len(lens), ptrs.ctypes.data, lens.ctypes.data,
+                                    last.ctypes.data, RC_OPEN if open_ else 0, cuts_ptr,
+                                    counts_ptr, stream or None))
+
+    def chunk_host(self, buffers, last_piece=None, open_=False):
+        """Chunk host streams (uint8 arrays / bytes-like); returns a list of cut-END arrays."""
+        arrs = [np.frombuffer(b, dtype=np.uint8) if not isinstance(b, np.ndarray) else b
+                for b in buffers]
+        n = len(arrs)
+        if n == 0:
+            return []
+        lens = _ptr_array([a.size for a in arrs])
+        ptrs = _ptr_array([a.ctypes.data if a.size else 0 for a in arrs])
+        last = _ptr_array(last_piece if last_piece is not None else np.zeros(n))
+        total, caps = self.capacity(lens)
+        cuts = np.zeros(max(total, 1), dtype=np.uint64)
+        counts = np.zeros(n, dtype=np.int64)
+        check(lib().rc_chunk_host(self._h, n, ptrs.ctypes.data, lens.ctypes.data,
+                                  last.ctypes.data, RC_OPEN if open_ else 0, cuts.ctypes.data,
+                                  counts.ctypes.data))
+        base = np.concatenate([[0], np.cumsum(caps)[:-1]]).astype(np.int64)
+        return [cuts[b:b + c] for b, c in zip(base, counts)]
+
+    # ---------------------------------------------------------------------- profiling
+
+    def timing(self, enable: bool):
+        check(lib().rc_timing_enable(self._h, 1 if enable else 0))
+
+    def read_timing(self):
+        a, b, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_uint64()
+        check(lib().rc_timing_read(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(n)))
+        return a.value, b.value, n.value
+
+
+def keys_needed(max_length, L, P):
+    return lib().rc_keys_needed(max_length, L, P)
+
+
+def fill_splitmix(ptr, nbytes, seed, stream_id, hip_stream=0):
+    check(lib().rc_fill_splitmix(ptr, nbytes, seed, stream_id, hip_stream or None))
+
+
+def tables_key(key16, ds):
+    ds = _ptr_array(ds)
+    out = np.zeros(len(ds), dtype=np.uint64)
+    top = np.zeros(len(ds), dtype=np.uint32)
+    check(lib().rc_tables_key(bytes(key16), len(ds), ds.ctypes.data, out.ctypes.data,
+                              top.ctypes.data))
+    return out, top
+
+
+def _current_device():
+    try:
+        import torch
+        if torch.cuda.is_available():
+            return torch.cuda.current_device()
+    except Exception:  # torch is optional plumbing
+        pass
+    return 0
+
+
+__all__ = ['GpuChunker', 'normalize_params', 'keys_needed', 'fill_splitmix', 'tables_key',
+           'MIN_LENGTH', 'MAX_LENGTH', '_lib']

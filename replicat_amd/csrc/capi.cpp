@@ -1,0 +1,624 @@
+// capi.cpp -- host side of the C ABI in include/replicat_chunker.h.
+//
+// Owns the per-key lookup tables (built here from k0/k1, see gclmul.h), per-call stream
+// descriptors, the tile-record workspace, and the blocking single-buffer `next_cut`
+// (the drop-in for /root/reference/src/adapters.cpp:42-70).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <array>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "../../include/replicat_chunker.h"
+#include "gclmul.h"
+
+using namespace rc;
+
+namespace {
+
+thread_local char g_err[512];
+
+int fail(int code, const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                  \
+    do {                                                                               \
+        const hipError_t e_ = (expr);                                                  \
+        if (e_ != hipSuccess)                                                          \
+            return fail(RC_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(e_));    \
+    } while (0)
+
+// Carry-less 64x64 -> 128 product.
+void clmul64(uint64_t a, uint64_t b, uint64_t &lo, uint64_t &hi) {
+    lo = hi = 0;
+    for (int i = 0; i < 64; ++i)
+        if ((b >> i) & 1) {
+            lo ^= a << i;
+            if (i) hi ^= a >> (64 - i);
+        }
+}
+
+// The linear part of the key map (adapters.cpp:72-77 without the k1 term).
+uint64_t key_linear(uint64_t k0, uint64_t d) {
+    uint64_t lo, hi, rlo, rhi;
+    clmul64(k0, d, lo, hi);
+    clmul64(0x1B, hi, rlo, rhi);  // single partial fold; the overflow bits rhi are dropped
+    return lo ^ rlo;
+}
+
+void build_tables(uint64_t k0, uint64_t k1, KeyTables &t) {
+    uint64_t col[64];
+    for (int c = 0; c < 64; ++c) col[c] = key_linear(k0, 1ull << c);
+    for (int b = 0; b < 4; ++b)
+        for (int v = 0; v < 256; ++v) {
+            uint64_t l = 0, h = 0;
+            for (int i = 0; i < 8; ++i)
+                if ((v >> i) & 1) {
+                    l ^= col[8 * b + i];
+                    h ^= col[32 + 8 * b + i];
+                }
+            if (b == 0) h ^= k1;
+            t.tl[b][v] = l;
+            t.th[b][v] = h;
+            t.pf[b][v] = (uint32_t)((l >> 48) << 16) | (uint32_t)(h >> 48);
+        }
+}
+
+uint64_t load_le64(const uint8_t *p) {
+    uint64_t v = 0;
+    for (int i = 7; i >= 0; --i) v = (v << 8) | p[i];
+    return v;
+}
+
+uint64_t window_keys(uint64_t max_length) { return max_length >= 1 ? (max_length - 1) / 4 : 0; }
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+// growable device buffer
+struct DevBuf {
+    void *p = nullptr;
+    size_t n = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= n) return 0;
+        if (p) {
+            HIP_TRY(hipDeviceSynchronize());
+            HIP_TRY(hipFree(p));
+            p = nullptr;
+            n = 0;
+        }
+        size_t want = std::max<size_t>(bytes, 4096);
+        want = (want + 4095) & ~(size_t)4095;
+        HIP_TRY(hipMalloc(&p, want));
+        n = want;
+        return 0;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
+struct HostBuf {  // growable pinned host buffer
+    void *p = nullptr;
+    size_t n = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= n) return 0;
+        if (p) HIP_TRY(hipHostFree(p));
+        p = nullptr;
+        n = 0;
+        size_t want = std::max<size_t>(bytes, 4096);
+        HIP_TRY(hipHostMalloc(&p, want, hipHostMallocDefault));
+        n = want;
+        return 0;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
+}  // namespace
+
+struct rc_chunker {
+    uint64_t min_length = 0, max_length = 0, window = 0;
+    uint64_t k0 = 0, k1 = 0;
+    int device = 0;
+    KeyTables tables;
+    KeyTables *d_tables = nullptr;
+    std::mutex mu;  // one call at a time per chunker (the reference is used by one thread)
+
+    // per-call workspaces, used alternately so that two calls can be in flight
+    struct Workspace {
+        HostBuf h_desc;     // pinned staging of the descriptor arrays
+        DevBuf d_desc;      // device copy
+        DevBuf d_records;   // one TileRecord per tile
+        hipEvent_t done = nullptr;  // the call that last used this workspace has finished
+        bool pending = false;
+    } ws[2];
+    unsigned next_ws = 0;
+
+    // single-buffer next_cut scratch
+    DevBuf d_buf, d_out;
+    HostBuf h_out;
+
+    // host-stream path scratch
+    DevBuf d_stage[2], d_hcuts[2], d_hcounts[2];
+    hipStream_t hstream[2] = {nullptr, nullptr};
+
+    // timing
+    bool timing = false;
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<std::array<hipEvent_t, 3>> ev_rec;
+};
+
+namespace {
+
+struct Plan {
+    uint64_t n = 0, n_tiles = 0, total_cap = 0;
+    size_t bytes = 0;
+};
+
+// Layout of the descriptor buffer: ptr[n] len[n] last[n] jneed[n] tile_base[n+1] cut_base[n]
+// cut_cap[n], all u64.
+StreamDesc desc_view(void *base, uint64_t n) {
+    uint64_t *u = static_cast<uint64_t *>(base);
+    StreamDesc d;
+    d.ptr = reinterpret_cast<const uint8_t *const *>(u);
+    d.len = u + n;
+    d.last = u + 2 * n;
+    d.jneed = u + 3 * n;
+    d.tile_base = u + 4 * n;
+    d.cut_base = u + 5 * n + 1;
+    d.cut_cap = u + 6 * n + 1;
+    return d;
+}
+
+uint64_t cut_cap_of(uint64_t min_length, uint64_t L) {
+    const uint64_t step = std::max<uint64_t>(4, (min_length + 3) & ~3ull);
+    return L / step + 3;
+}
+
+int validate_streams(uint64_t n, const uint8_t *const *ptrs, const uint64_t *lens,
+                     const uint64_t *last, bool device_aligned) {
+    if (n && (!ptrs || !lens)) return fail(RC_ERR_ARGUMENT, "null stream arrays");
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t P = last ? last[i] : 0;
+        if (P > lens[i]) return fail(RC_ERR_ARGUMENT, "stream %llu: last piece start %llu > length %llu",
+                                     (unsigned long long)i, (unsigned long long)P,
+                                     (unsigned long long)lens[i]);
+        if (lens[i] && !ptrs[i]) return fail(RC_ERR_ARGUMENT, "stream %llu: null pointer", (unsigned long long)i);
+        if (device_aligned && lens[i] && (reinterpret_cast<uintptr_t>(ptrs[i]) & 15))
+            return fail(RC_ERR_ALIGN, "stream %llu: device pointer not 16-byte aligned",
+                        (unsigned long long)i);
+    }
+    return 0;
+}
+
+// Fill the pinned descriptor staging and return the plan.  Waits for the previous upload
+// from the same staging to have been consumed.
+using Workspace = rc_chunker::Workspace;
+
+Workspace &acquire_ws(rc_chunker *ch) {
+    Workspace &w = ch->ws[ch->next_ws & 1];
+    ++ch->next_ws;
+    return w;
+}
+
+int stage_descriptors(rc_chunker *ch, Workspace &ws, uint64_t n, const uint8_t *const *ptrs,
+                      const uint64_t *lens, const uint64_t *last, Plan &plan, bool open = false) {
+    plan.n = n;
+    plan.bytes = (7 * n + 1) * sizeof(uint64_t);
+    if (ws.pending) {  // the call that used this workspace before must be done with it
+        HIP_TRY(hipEventSynchronize(ws.done));
+        ws.pending = false;
+    }
+    if (int rc = ws.h_desc.ensure(plan.bytes)) return rc;
+    uint64_t *u = static_cast<uint64_t *>(ws.h_desc.p);
+    uint64_t tiles = 0, cuts = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t L = lens[i], P = open ? L : (last ? last[i] : 0);
+        const uint64_t jneed = rc_keys_needed(ch->max_length, L, P);
+        u[i] = reinterpret_cast<uint64_t>(ptrs[i]);
+        u[n + i] = L;
+        u[2 * n + i] = P;
+        u[3 * n + i] = jneed;
+        u[4 * n + i] = tiles;
+        tiles += jneed ? jneed / kTileKeys + 1 : 0;
+        const uint64_t cap = cut_cap_of(ch->min_length, L);
+        u[5 * n + 1 + i] = cuts;
+        u[6 * n + 1 + i] = cap;
+        cuts += cap;
+    }
+    u[5 * n] = tiles;
+    plan.n_tiles = tiles;
+    plan.total_cap = cuts;
+    return 0;
+}
+
+int upload_and_launch(rc_chunker *ch, Workspace &ws, const Plan &plan, ChainParams prm,
+                      uint64_t *d_cuts, int64_t *d_counts, hipStream_t stream) {
+    if (int rc = ws.d_desc.ensure(plan.bytes)) return rc;
+    if (int rc = ws.d_records.ensure(std::max<uint64_t>(plan.n_tiles, 1) * sizeof(TileRecord)))
+        return rc;
+    HIP_TRY(hipMemcpyAsync(ws.d_desc.p, ws.h_desc.p, plan.bytes, hipMemcpyHostToDevice, stream));
+    const StreamDesc d = desc_view(ws.d_desc.p, plan.n);
+    std::array<hipEvent_t, 3> ev{};
+    if (ch->timing) {
+        for (auto &e : ev) {
+            if (ch->ev_pool.empty()) {
+                HIP_TRY(hipEventCreate(&e));
+            } else {
+                e = ch->ev_pool.back();
+                ch->ev_pool.pop_back();
+            }
+        }
+        HIP_TRY(hipEventRecord(ev[0], stream));
+    }
+    if (rc_launch_tiles(ch->d_tables, d, plan.n, plan.n_tiles,
+                        static_cast<TileRecord *>(ws.d_records.p), stream))
+        return fail(RC_ERR_HIP, "%s", rc_launch_error());
+    if (ch->timing) HIP_TRY(hipEventRecord(ev[1], stream));
+    if (rc_launch_chain(ch->d_tables, d, plan.n, prm,
+                        static_cast<const TileRecord *>(ws.d_records.p), d_cuts, d_counts,
+                        stream))
+        return fail(RC_ERR_HIP, "%s", rc_launch_error());
+    HIP_TRY(hipEventRecord(ws.done, stream));
+    ws.pending = true;
+    if (ch->timing) {
+        HIP_TRY(hipEventRecord(ev[2], stream));
+        ch->ev_rec.push_back(ev);
+    }
+    return 0;
+}
+
+ChainParams chain_params(const rc_chunker *ch, uint64_t max_steps, uint32_t flags = 0) {
+    ChainParams p;
+    p.open = (flags & RC_OPEN) ? 1u : 0u;
+    p.min_length = ch->min_length;
+    p.max_length = ch->max_length;
+    p.window = ch->window;
+    p.max_steps = max_steps;
+    return p;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rc_version(void) { return 100; }
+
+const char *rc_last_error(void) { return g_err; }
+
+uint64_t rc_keys_needed(uint64_t max_length, uint64_t L, uint64_t P) {
+    // S4: at chunk start s an argmax happens iff P - s >= max or L - s >= 2*max; the window of
+    // start s reaches key s/4 + T (adapters.cpp:59).  Largest such s -> largest key.
+    const uint64_t T = window_keys(max_length);
+    if (T == 0 || L < 8) return 0;
+    bool any = false;
+    uint64_t bound = 0;
+    if (P >= max_length) {
+        any = true;
+        bound = P - max_length;
+    }
+    if (L >= 2 * max_length) {
+        const uint64_t b2 = L - 2 * max_length;
+        if (!any || b2 > bound) bound = b2;
+        any = true;
+    }
+    if (!any) return 0;
+    const uint64_t jneed = bound / 4 + T, jmax = (L - 4) / 4;
+    return std::min(jneed, jmax);
+}
+
+int rc_chunker_create(uint64_t min_length, uint64_t max_length, const uint8_t *key,
+                      uint64_t key_len, int device, rc_chunker **out) {
+    if (!out) return fail(RC_ERR_ARGUMENT, "null output handle");
+    *out = nullptr;
+    // adapters.cpp:21-29, in the reference's order
+    if (key_len != 16 || !key) return fail(RC_ERR_KEY_LENGTH, "key must contain exactly 16 characters");
+    if (min_length > max_length)
+        return fail(RC_ERR_MIN_GT_MAX, "Minimum length is greater than the maximum one");
+    const uint64_t k0 = load_le64(key), k1 = load_le64(key + 8);
+    if (k0 == 0) return fail(RC_ERR_BAD_KEY, "Bad key contents");
+
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return fail(RC_ERR_NO_DEVICE, "no HIP device available (the chunker runs on MI355X only)");
+    if (device < 0 || device >= ndev) return fail(RC_ERR_NO_DEVICE, "device %d out of range", device);
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(RC_ERR_NO_DEVICE, "device %d is %s, not gfx950", device, prop.gcnArchName);
+
+    rc_chunker *ch = new rc_chunker();
+    ch->min_length = min_length;
+    ch->max_length = max_length;
+    ch->window = window_keys(max_length);
+    ch->k0 = k0;
+    ch->k1 = k1;
+    ch->device = device;
+    build_tables(k0, k1, ch->tables);
+    {
+        DeviceGuard g(device);
+        hipError_t e = hipMalloc(&ch->d_tables, sizeof(KeyTables));
+        if (e == hipSuccess)
+            e = hipMemcpy(ch->d_tables, &ch->tables, sizeof(KeyTables), hipMemcpyHostToDevice);
+        for (auto &w : ch->ws)
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&w.done, hipEventDisableTiming);
+        if (e != hipSuccess) {
+            rc_chunker_destroy(ch);
+            return fail(RC_ERR_HIP, "device setup failed: %s", hipGetErrorString(e));
+        }
+    }
+    *out = ch;
+    return RC_OK;
+}
+
+void rc_chunker_destroy(rc_chunker *ch) {
+    if (!ch) return;
+    {
+        DeviceGuard g(ch->device);
+        (void)hipDeviceSynchronize();
+        if (ch->d_tables) (void)hipFree(ch->d_tables);
+        for (auto &w : ch->ws) {
+            w.d_desc.release();
+            w.d_records.release();
+            w.h_desc.release();
+            if (w.done) (void)hipEventDestroy(w.done);
+        }
+        ch->d_buf.release();
+        ch->d_out.release();
+        for (int i = 0; i < 2; ++i) {
+            ch->d_stage[i].release();
+            ch->d_hcuts[i].release();
+            ch->d_hcounts[i].release();
+            if (ch->hstream[i]) (void)hipStreamDestroy(ch->hstream[i]);
+        }
+        ch->h_out.release();
+        for (auto &r : ch->ev_rec)
+            for (auto e : r) (void)hipEventDestroy(e);
+        for (auto e : ch->ev_pool) (void)hipEventDestroy(e);
+    }
+    delete ch;
+}
+
+uint64_t rc_chunker_min_length(const rc_chunker *ch) { return ch ? ch->min_length : 0; }
+uint64_t rc_chunker_max_length(const rc_chunker *ch) { return ch ? ch->max_length : 0; }
+
+uint64_t rc_host_key(const rc_chunker *ch, uint64_t d) {
+    const uint32_t lo = (uint32_t)d, hi = (uint32_t)(d >> 32);
+    uint64_t k = 0;
+    for (int b = 0; b < 4; ++b) k ^= ch->tables.tl[b][(lo >> (8 * b)) & 255] ^ ch->tables.th[b][(hi >> (8 * b)) & 255];
+    return k;
+}
+
+int rc_tables_key(const uint8_t *key16, uint64_t n, const uint64_t *ds, uint64_t *out,
+                  uint32_t *top16) {
+    if (!key16 || (n && (!ds || !out))) return fail(RC_ERR_ARGUMENT, "null argument");
+    KeyTables *t = new KeyTables;
+    build_tables(load_le64(key16), load_le64(key16 + 8), *t);
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint32_t lo = (uint32_t)ds[i], hi = (uint32_t)(ds[i] >> 32);
+        uint64_t k = 0;
+        uint32_t el = 0, eh = 0;
+        for (int b = 0; b < 4; ++b) {
+            k ^= t->tl[b][(lo >> (8 * b)) & 255] ^ t->th[b][(hi >> (8 * b)) & 255];
+            el ^= t->pf[b][(lo >> (8 * b)) & 255];
+            eh ^= t->pf[b][(hi >> (8 * b)) & 255];
+        }
+        out[i] = k;
+        // the kernel's combination: (e(w[j-1]) & 0xffff0000) ^ (e(w[j]) << 16)
+        if (top16) top16[i] = ((el & 0xffff0000u) ^ (eh << 16)) >> 16;
+    }
+    delete t;
+    return RC_OK;
+}
+
+uint64_t rc_cut_capacity(const rc_chunker *ch, uint64_t n, const uint64_t *lens, uint64_t *caps) {
+    uint64_t total = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t c = cut_cap_of(ch->min_length, lens[i]);
+        if (caps) caps[i] = c;
+        total += c;
+    }
+    return total;
+}
+
+int rc_next_cut(rc_chunker *ch, const uint8_t *buffer, uint64_t size, int final, uint64_t *out_cut) {
+    if (!ch || !out_cut) return fail(RC_ERR_ARGUMENT, "null argument");
+    if (size && !buffer) return fail(RC_ERR_ARGUMENT, "null buffer");
+    const uint64_t mn = ch->min_length, mx = ch->max_length;
+    // adapters.cpp:48-57
+    if (final && size < 2 * mx) {
+        *out_cut = size <= mx ? size : (size < mx + mn ? size / 2 : mx);
+        return RC_OK;
+    }
+    if (!final && size < mx) {
+        *out_cut = 0;
+        return RC_OK;
+    }
+    if (ch->window == 0) {  // no key offsets below max: adapters.cpp:66-67 directly
+        *out_cut = (mn + 3) & ~3ull;
+        return RC_OK;
+    }
+    std::lock_guard<std::mutex> lock(ch->mu);
+    DeviceGuard g(ch->device);
+    // keys 1..T read bytes [0, 4T+4); never more than the buffer holds
+    const uint64_t ncopy = std::min<uint64_t>(size, 4 * ch->window + 4);
+    if (int rc = ch->d_buf.ensure(ncopy + 16)) return rc;
+    if (int rc = ch->d_out.ensure(64)) return rc;
+    if (int rc = ch->h_out.ensure(64)) return rc;
+    hipStream_t stream = nullptr;
+    HIP_TRY(hipMemcpyAsync(ch->d_buf.p, buffer, ncopy, hipMemcpyHostToDevice, stream));
+    const uint8_t *ptr = static_cast<const uint8_t *>(ch->d_buf.p);
+    const uint64_t L = ncopy, P = ncopy;
+    Plan plan;
+    Workspace &ws = acquire_ws(ch);
+    if (int rc = stage_descriptors(ch, ws, 1, &ptr, &L, &P, plan)) return rc;
+    uint64_t *d_cut = static_cast<uint64_t *>(ch->d_out.p);
+    int64_t *d_count = reinterpret_cast<int64_t *>(d_cut + 1);
+    const bool timing = ch->timing;
+    ch->timing = false;
+    int rc = upload_and_launch(ch, ws, plan, chain_params(ch, 0), d_cut, d_count, stream);
+    ch->timing = timing;
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(ch->h_out.p, d_cut, 16, hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    const uint64_t *h = static_cast<const uint64_t *>(ch->h_out.p);
+    if ((int64_t)h[1] != 1) return fail(RC_ERR_OVERFLOW, "device chain returned %lld cuts", (long long)h[1]);
+    *out_cut = h[0];
+    return RC_OK;
+}
+
+int rc_chunk_device(rc_chunker *ch, uint64_t n, const uint8_t *const *d_streams,
+                    const uint64_t *lens, const uint64_t *last_piece, uint32_t flags,
+                    uint64_t *d_cuts, int64_t *d_counts, void *hip_stream) {
+    if (!ch) return fail(RC_ERR_ARGUMENT, "null chunker");
+    if (n == 0) return RC_OK;
+    if (!d_cuts || !d_counts) return fail(RC_ERR_ARGUMENT, "null output arrays");
+    const bool open = (flags & RC_OPEN) != 0;
+    if (int rc = validate_streams(n, d_streams, lens, open ? nullptr : last_piece, true)) return rc;
+    std::lock_guard<std::mutex> lock(ch->mu);
+    DeviceGuard g(ch->device);
+    Plan plan;
+    Workspace &ws = acquire_ws(ch);
+    if (int rc = stage_descriptors(ch, ws, n, d_streams, lens, last_piece, plan, open)) return rc;
+    return upload_and_launch(ch, ws, plan, chain_params(ch, ~0ull, flags), d_cuts, d_counts,
+                             static_cast<hipStream_t>(hip_stream));
+}
+
+int rc_chunk_host(rc_chunker *ch, uint64_t n, const uint8_t *const *streams, const uint64_t *lens,
+                  const uint64_t *last_piece, uint32_t flags, uint64_t *cuts, int64_t *counts) {
+    if (!ch) return fail(RC_ERR_ARGUMENT, "null chunker");
+    if (n == 0) return RC_OK;
+    if (!cuts || !counts) return fail(RC_ERR_ARGUMENT, "null output arrays");
+    const bool open = (flags & RC_OPEN) != 0;
+    if (int rc = validate_streams(n, streams, lens, open ? nullptr : last_piece, false)) return rc;
+    std::lock_guard<std::mutex> lock(ch->mu);
+    DeviceGuard g(ch->device);
+    for (int i = 0; i < 2; ++i)
+        if (!ch->hstream[i]) HIP_TRY(hipStreamCreateWithFlags(&ch->hstream[i], hipStreamNonBlocking));
+
+    // batches of whole streams, each up to `budget` bytes (one stream may exceed it alone)
+    const uint64_t budget = 1ull << 30;
+    std::vector<uint64_t> cut_base(n + 1, 0);
+    for (uint64_t i = 0; i < n; ++i) cut_base[i + 1] = cut_base[i] + cut_cap_of(ch->min_length, lens[i]);
+
+    struct Batch {
+        uint64_t first = 0, count = 0;
+    } inflight[2];
+    bool busy[2] = {false, false};
+    std::vector<const uint8_t *> dptr;
+    std::vector<uint64_t> off;
+
+    auto finish = [&](int slot) -> int {
+        if (!busy[slot]) return 0;
+        HIP_TRY(hipStreamSynchronize(ch->hstream[slot]));
+        busy[slot] = false;
+        const Batch &b = inflight[slot];
+        for (uint64_t i = 0; i < b.count; ++i)
+            if (counts[b.first + i] < 0)
+                return fail(RC_ERR_OVERFLOW, "stream %llu overflowed its cut capacity",
+                            (unsigned long long)(b.first + i));
+        return 0;
+    };
+
+    uint64_t i = 0;
+    int slot = 0;
+    while (i < n) {
+        uint64_t j = i, bytes = 0;
+        while (j < n && (j == i || bytes + ((lens[j] + 15) & ~15ull) <= budget)) {
+            bytes += (lens[j] + 15) & ~15ull;
+            ++j;
+        }
+        if (int rc = finish(slot)) return rc;  // slot's previous batch done: buffers free
+        const uint64_t nb = j - i;
+        if (int rc = ch->d_stage[slot].ensure(bytes + 16)) return rc;
+        const uint64_t ncut = cut_base[j] - cut_base[i];
+        if (int rc = ch->d_hcuts[slot].ensure(ncut * 8)) return rc;
+        if (int rc = ch->d_hcounts[slot].ensure(nb * 8)) return rc;
+        hipStream_t st = ch->hstream[slot];
+        dptr.resize(nb);
+        uint64_t o = 0;
+        for (uint64_t k = 0; k < nb; ++k) {
+            uint8_t *dst = static_cast<uint8_t *>(ch->d_stage[slot].p) + o;
+            dptr[k] = dst;
+            if (lens[i + k]) HIP_TRY(hipMemcpyAsync(dst, streams[i + k], lens[i + k], hipMemcpyHostToDevice, st));
+            o += (lens[i + k] + 15) & ~15ull;
+        }
+        Plan plan;
+        Workspace &ws = acquire_ws(ch);
+        if (int rc = stage_descriptors(ch, ws, nb, dptr.data(), lens + i,
+                                       last_piece ? last_piece + i : nullptr, plan, open))
+            return rc;
+        uint64_t *dc = static_cast<uint64_t *>(ch->d_hcuts[slot].p);
+        int64_t *dn = static_cast<int64_t *>(ch->d_hcounts[slot].p);
+        if (int rc = upload_and_launch(ch, ws, plan, chain_params(ch, ~0ull, flags), dc, dn, st))
+            return rc;
+        HIP_TRY(hipMemcpyAsync(cuts + cut_base[i], dc, ncut * 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(counts + i, dn, nb * 8, hipMemcpyDeviceToHost, st));
+        inflight[slot] = {i, nb};
+        busy[slot] = true;
+        i = j;
+        slot ^= 1;
+    }
+    if (int rc = finish(0)) return rc;
+    if (int rc = finish(1)) return rc;
+    return RC_OK;
+}
+
+int rc_timing_enable(rc_chunker *ch, int enable) {
+    if (!ch) return fail(RC_ERR_ARGUMENT, "null chunker");
+    ch->timing = enable != 0;
+    return RC_OK;
+}
+
+int rc_timing_read(rc_chunker *ch, double *phase_a_ms, double *phase_b_ms, uint64_t *calls) {
+    if (!ch) return fail(RC_ERR_ARGUMENT, "null chunker");
+    std::lock_guard<std::mutex> lock(ch->mu);
+    DeviceGuard g(ch->device);
+    double a = 0, b = 0;
+    for (auto &r : ch->ev_rec) {
+        HIP_TRY(hipEventSynchronize(r[2]));
+        float x = 0, y = 0;
+        HIP_TRY(hipEventElapsedTime(&x, r[0], r[1]));
+        HIP_TRY(hipEventElapsedTime(&y, r[1], r[2]));
+        a += x;
+        b += y;
+        for (auto e : r) ch->ev_pool.push_back(e);
+    }
+    if (phase_a_ms) *phase_a_ms = a;
+    if (phase_b_ms) *phase_b_ms = b;
+    if (calls) *calls = ch->ev_rec.size();
+    ch->ev_rec.clear();
+    return RC_OK;
+}
+
+int rc_fill_splitmix(uint8_t *d_dst, uint64_t nbytes, uint64_t seed, uint64_t stream, void *hip_stream) {
+    if (nbytes && !d_dst) return fail(RC_ERR_ARGUMENT, "null destination");
+    if (rc_launch_fill(d_dst, nbytes, seed, stream, hip_stream)) return fail(RC_ERR_HIP, "%s", rc_launch_error());
+    return RC_OK;
+}
+
+}  // extern "C"

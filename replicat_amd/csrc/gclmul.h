@@ -1,0 +1,86 @@
+// gclmul.h -- layouts shared by the gfx950 kernels (kernels.hip) and the host side (capi.cpp).
+//
+// Key algebra (replaces the PCLMULQDQ pair of /root/reference/src/adapters.cpp:72-77).
+// gfx950 has no carry-less multiply, but for a fixed key the chunker hash is GF(2)-affine
+// in the 8 data bytes:  key(d) = k1 ^ M d,  M a 64x64 bit matrix fixed by k0.  Key j of a
+// stream covers bytes [4j-4, 4j+4) = LE32 words w[j-1] (low half) and w[j] (high half), so
+//     key(j) = k1 ^ Lmap(w[j-1]) ^ Hmap(w[j])
+// with Lmap/Hmap the two 32-column halves of M.  Each is evaluated one byte at a time from
+// 256-entry tables:   TL[b][v] = Lmap(v << 8b),  TH[b][v] = Hmap(v << 8b)  (k1 folded into TH[0]).
+// The streaming kernel needs only the TOP 16 bits of every key to find each lane's candidate
+// (the exact 64-bit key is evaluated once per lane and tile), so it uses 32-bit
+// "prefilter" entries  PF[b][v] = top16(TL[b][v]) << 16 | top16(TH[b][v]).
+#pragma once
+#include <stdint.h>
+
+namespace rc {
+
+constexpr int kTileKeys = 4096;      // keys per tile = one wave: 64 lanes x 16 iters x 4 keys
+constexpr int kTileIters = 16;       // 16-byte loads per lane per tile
+constexpr int kWaveSize = 64;
+constexpr int kTileWaves = 16;       // waves per workgroup of the tile kernel (1024 threads)
+constexpr int kChainWaves = 4;       // waves (= streams) per workgroup of the chain kernel
+
+// ---- LDS image of the tile kernel -------------------------------------------------------
+// Prefilter tables replicated 32x so that the 32 lanes of each ds_read_b32 lane group each own
+// one bank (bank = dword address mod 32 = lane mod 32): conflict-free random lookups.
+//   byte address of PF[b][v] for lane l:  (b>>1)*65536 + v*256 + (b&1)*128 + (l&31)*4
+constexpr uint32_t kPfBytes = 131072;
+constexpr uint32_t kFullOff = kPfBytes;                 // TL[4][256], then TH[4][256] (u64)
+constexpr uint32_t kFullBytes = 2 * 4 * 256 * 8;        // 16 KiB
+constexpr uint32_t kTileLdsBytes = kPfBytes + kFullBytes;
+
+// Key tables of one chunker, built on the host, uploaded once, staged into LDS per workgroup.
+struct KeyTables {
+    uint64_t tl[4][256];
+    uint64_t th[4][256];   // k1 folded into th[0][*]
+    uint32_t pf[4][256];
+};
+
+// Per-call stream descriptors (structure of arrays in one device buffer).
+struct StreamDesc {
+    const uint8_t *const *ptr;  // device pointers
+    const uint64_t *len;        // L
+    const uint64_t *last;       // P
+    const uint64_t *jneed;      // last key any window can reach (0 = none)
+    const uint64_t *tile_base;  // n+1 entries, exclusive prefix sum of tiles per stream
+    const uint64_t *cut_base;   // n entries
+    const uint64_t *cut_cap;    // n entries
+};
+
+// One record per tile: first maximal key of the tile and its key index in the stream.
+struct TileRecord {
+    uint64_t key;
+    uint64_t j;
+};
+
+struct ChainParams {
+    uint64_t min_length;
+    uint64_t max_length;
+    uint64_t window;      // T = (max_length - 1) / 4 keys per argmax window (0 if max < 5)
+    uint64_t max_steps;   // stop after this many cuts per stream (~0 = unbounded; 0 = one raw
+                          // argmax whatever its value: the single-buffer next_cut)
+    uint32_t open;        // RC_OPEN: non-final prefix, no tail rule
+};
+
+// splitmix64 finaliser (replicat_amd/synth.py)
+__host__ __device__ inline uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+}  // namespace rc
+
+// Launchers implemented in kernels.hip (host-callable, enqueue only).
+extern "C" {
+int rc_launch_tiles(const rc::KeyTables *d_tables, rc::StreamDesc desc, uint64_t n_streams,
+                    uint64_t n_tiles, rc::TileRecord *d_records, void *stream);
+int rc_launch_chain(const rc::KeyTables *d_tables, rc::StreamDesc desc, uint64_t n_streams,
+                    rc::ChainParams prm, const rc::TileRecord *d_records, uint64_t *d_cuts,
+                    int64_t *d_counts, void *stream);
+int rc_launch_fill(uint8_t *d_dst, uint64_t nbytes, uint64_t seed, uint64_t stream_id,
+                   void *stream);
+const char *rc_launch_error(void);
+}

@@ -1,0 +1,232 @@
+"""GPU parity: the HIP chunker (through the C ABI) against the reference's golden outputs and
+the oracle, bit for bit.  Runs on an MI355X only (-m gpu)."""
+import random
+
+import numpy as np
+import pytest
+
+import golden_util as G
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip('torch')
+if not torch.cuda.is_available():  # pragma: no cover - CPU container
+    pytest.skip('needs an MI355X', allow_module_level=True)
+
+from gpu_util import chunk_device, device_streams  # noqa: E402
+
+from replicat_amd import synth  # noqa: E402
+from replicat_amd._replicat_adapters import _gclmulchunker  # noqa: E402
+from replicat_amd.adapters import gclmulchunker as BatchedChunker  # noqa: E402
+from replicat_amd.chunker import GpuChunker, normalize_params  # noqa: E402
+
+SMALL = G.load('small_cases.json')
+KNOWN = G.load('known_answers.json')
+STREAMS = G.load('streams.json')
+DIGESTS = G.load('digests.json')
+
+
+def loop_next_cut(pieces, min_length, max_length, params):
+    """replicat's adapter loop (replicat/utils/adapters.py:290-305) over the drop-in
+    `_gclmulchunker`: the reference's caller, unchanged, on top of the HIP module."""
+    chunker = _gclmulchunker(min_length, max_length, normalize_params(params))
+    buffer = bytearray()
+    sizes = []
+    it = iter(pieces)
+    chunk = next(it, None)
+    while chunk is not None:
+        buffer += chunk
+        nxt = next(it, None)
+        while True:
+            pos = chunker.next_cut(buffer, bool(nxt is None))
+            if not pos:
+                break
+            sizes.append(pos)
+            del buffer[:pos]
+        chunk = nxt
+    return sizes
+
+
+def batched(pieces, min_length, max_length, params, batch_bytes):
+    c = BatchedChunker(min_length=min_length, max_length=max_length, batch_bytes=batch_bytes)
+    out = list(c(pieces, params=params))
+    assert b''.join(out) == b''.join(pieces)
+    return [len(x) for x in out]
+
+
+@pytest.mark.parametrize('idx', range(0, len(SMALL), 3))
+def test_small_cases_next_cut_loop(idx):
+    case = SMALL[idx]
+    if case['max'] % 4 and len(case['pieces']) > 1:
+        pytest.skip('outside the parity domain (SURVEY.md §8 a0 S7)')
+    got = loop_next_cut(G.case_pieces(case), case['min'], case['max'], G.params_of(case))
+    assert got == case['expected']
+
+
+def test_small_cases_device_batch():
+    """All small cases in ONE rc_chunk_device call (mixed lengths / framings per stream)."""
+    cases = [c for c in SMALL if c['max'] % 4 == 0 or len(c['pieces']) <= 1]
+    by_params = {}
+    for c in cases:
+        by_params.setdefault((c['min'], c['max'], normalize_params(G.params_of(c))), []).append(c)
+    for (mn, mx, key), group in by_params.items():
+        ch = GpuChunker(mn, mx, key)
+        datas = [np.frombuffer(b''.join(G.case_pieces(c)), np.uint8) for c in group]
+        sizes = [c['size'] for c in group]
+        last = [c['size'] - c['pieces'][-1] if c['pieces'] else 0 for c in group]
+        ts = device_streams(sizes, datas=datas)
+        ends = chunk_device(ch, ts, sizes, last)
+        for c, e in zip(group, ends):
+            assert [b - a for a, b in zip([0] + e[:-1], e)] == c['expected']
+
+
+@pytest.mark.parametrize('batch_bytes', [1 << 12, 1 << 16, 1 << 28])
+def test_small_cases_batched_adapter(batch_bytes):
+    for case in SMALL[::2]:
+        if case['max'] % 4:
+            continue
+        got = batched(G.case_pieces(case), case['min'], case['max'], G.params_of(case),
+                      batch_bytes)
+        assert got == case['expected'], case
+
+
+@pytest.mark.parametrize('idx', range(len(KNOWN['alignment'])))
+def test_known_alignment(idx):
+    c = KNOWN['alignment'][idx]
+    pieces = [bytes([c['byte']]) * n for n in c['pieces']]
+    assert loop_next_cut(pieces, c['min'], c['max'], None) == c['expected']
+    if c['max'] % 4 == 0:
+        assert batched(pieces, c['min'], c['max'], None, 1) == c['expected']
+
+
+@pytest.mark.parametrize('idx', range(len(KNOWN['seeded'])))
+def test_known_seeded(idx):
+    c = KNOWN['seeded'][idx]
+    pieces = G.seeded_inputs(c)
+    params = bytes.fromhex(c['params'])
+    assert batched(pieces, 500, 10_000, params, 1 << 20) == c['expected']
+    if c['repeat'] == 1:
+        assert loop_next_cut(pieces, 500, 10_000, params) == c['expected']
+    if 'expected_after_flip0' in c:
+        data = bytearray(pieces[0])
+        data[0] = (data[0] - 1) % 255
+        assert batched([bytes(data)], 500, 10_000, params, 1 << 20) == c['expected_after_flip0']
+
+
+def test_golden_streams_device():
+    """streams.json: 64 MiB streams, 16 MiB piece framing, zero / constant data, 1 MiB."""
+    groups = {}
+    for e in STREAMS:
+        key = normalize_params(None if e['params'] is None else bytes.fromhex(e['params']))
+        groups.setdefault((e['min'], e['max'], key), []).append(e)
+    for (mn, mx, key), es in groups.items():
+        ch = GpuChunker(mn, mx, key)
+        ts, sizes, last = [], [], []
+        for e in es:
+            sizes.append(e['size'])
+            last.append(G.last_piece_start(e['size'], e['piece']))
+            if e['data'][0] == 'splitmix':
+                ts += device_streams([e['size']], seed=e['data'][1], ids=[e['data'][2]])
+            else:
+                ts += device_streams([e['size']], fill=e['data'][1])
+        got = chunk_device(ch, ts, sizes, last)
+        for e, g in zip(es, got):
+            assert g == e['ends'], (e['data'], e['size'])
+
+
+@pytest.mark.parametrize('name', [d['name'] for d in DIGESTS])
+def test_full_size_digests(name):
+    """Full configuration sizes, device-generated bytes: SHA-256 of all cut lists equals the
+    reference's (config 2 = 1024 x 64 MiB, 64 GiB resident in HBM)."""
+    d = next(x for x in DIGESTS if x['name'] == name)
+    key = normalize_params(None if d['params'] is None else bytes.fromhex(d['params']))
+    ch = GpuChunker(d['min'], d['max'], key)
+    all_ends = []
+    per_call = max(1, (16 << 30) // d['size'])
+    for first in range(0, d['streams'], per_call):
+        ids = list(range(first, min(d['streams'], first + per_call)))
+        ts = device_streams([d['size']] * len(ids), seed=d['seed'], ids=ids)
+        all_ends += chunk_device(ch, ts, [d['size']] * len(ids))
+        del ts
+        torch.cuda.empty_cache()
+    assert sum(map(len, all_ends)) == d['chunks']
+    assert G.cutlist_digest(all_ends) == d['sha256']
+
+
+def _oracle():
+    from oracle import oracle as o
+    o.lib()
+    return o
+
+
+@pytest.mark.parametrize('seed', range(6))
+def test_random_vs_oracle(seed):
+    """Random params/framing/data (incl. long runs of equal keys) against the oracle."""
+    o = _oracle()
+    rnd = random.Random(seed)
+    mx = rnd.choice([8, 64, 4096, 16384 + 4, 65536, 1 << 20])
+    mn = rnd.randrange(1, mx + 1)
+    key = rnd.randbytes(16)
+    if key[:8] == bytes(8):
+        key = b'\x01' + key[1:]
+    ch = GpuChunker(mn, mx, key)
+    sizes, datas, last = [], [], []
+    for _ in range(24):
+        n = rnd.choice([0, 3, 8, mx, 2 * mx, 2 * mx + 5, rnd.randrange(0, 40 * mx + 1),
+                        rnd.randrange(0, 8 << 20)])
+        kind = rnd.random()
+        if kind < 0.7:
+            d = np.frombuffer(rnd.randbytes(n), np.uint8)
+        elif kind < 0.8:
+            d = np.zeros(n, np.uint8)
+        else:
+            unit = np.frombuffer(rnd.randbytes(rnd.randrange(1, 64)), np.uint8)
+            d = np.resize(unit, n)
+        sizes.append(n)
+        datas.append(d)
+        last.append(rnd.choice([0, n, rnd.randrange(0, n + 1)]))
+    ts = device_streams(sizes, datas=datas)
+    got = chunk_device(ch, ts, sizes, last)
+    for d, P, g in zip(datas, last, got):
+        assert g == o.chunk_stream(d, mn, mx, key, P)
+
+
+def test_open_prefix_matches_nonfinal_calls():
+    """RC_OPEN: cuts only while L - s >= max (the adapter's non-final next_cut calls)."""
+    o = _oracle()
+    mn, mx = 500, 10_000
+    key = b'\x5a' * 16
+    ch = GpuChunker(mn, mx, key)
+    rnd = random.Random(7)
+    data = np.frombuffer(rnd.randbytes(3_000_000), np.uint8)
+    ts = device_streams([data.size], datas=[data])
+    got = chunk_device(ch, ts, [data.size], None, open_=True)[0]
+    full = o.chunk_stream(data, mn, mx, key, data.size)  # P = L: argmax iff L - s >= max
+    exp = []
+    s = 0
+    for e in full:
+        if data.size - s < mx:
+            break
+        exp.append(e)
+        s = e
+    assert got == exp
+
+
+def test_misaligned_and_bad_framing_rejected():
+    ch = GpuChunker(500, 10_000, b'\xff' * 16)
+    t = torch.zeros(1024, dtype=torch.uint8, device='cuda')
+    from replicat_amd._lib import ChunkerError
+    with pytest.raises(ChunkerError):
+        ch.chunk_device([t.data_ptr() + 4], [100], [0], t.data_ptr(), t.data_ptr(), 0)
+    with pytest.raises(ChunkerError):
+        ch.chunk_device([t.data_ptr()], [100], [101], t.data_ptr(), t.data_ptr(), 0)
+
+
+def test_host_path_matches_device():
+    ch = GpuChunker(128_000, 5_120_000, b'\xff' * 16)
+    bufs = [synth.stream_bytes(n, synth.DEFAULT_SEED, i)
+            for i, n in enumerate([64 << 20, 0, 5, 11 << 20, 48 << 20])]
+    o = _oracle()
+    got = ch.chunk_host(bufs)
+    for b, g in zip(bufs, got):
+        assert g.tolist() == o.chunk_stream(b, 128_000, 5_120_000, None, 0)
