@@ -115,6 +115,17 @@ uint64_t rc_keys_needed(uint64_t max_length, uint64_t L, uint64_t P);
 /* One 64-bit key of the chunker on the host, from its lookup tables (tests / tooling). */
 uint64_t rc_host_key(const rc_chunker *ch, uint64_t d);
 
+/* Inspection (tests): run only the per-tile phase (tile + edge kernels) over device streams and
+ * copy the tile records to host arrays: for tile t of the concatenated tile list (stream i's
+ * tiles start at the exclusive prefix sum of ceil((jneed_i + 1) / rc_tile_keys())), keys[t] =
+ * the first maximal 64-bit key among the tile's needed keys (0 if none is positive) and
+ * js[t] = its key index in the stream.  *n_tiles receives the tile count; at most cap are
+ * copied.  Blocking. */
+int rc_tile_records(rc_chunker *ch, uint64_t n, const uint8_t *const *d_streams,
+                    const uint64_t *lens, const uint64_t *last_piece, uint64_t *keys,
+                    uint64_t *js, uint64_t cap, uint64_t *n_tiles);
+uint64_t rc_tile_keys(void);
+
 /* Host-only check of the table construction (no device needed): out[i] = key of data word
  * ds[i] under the 16-byte key, evaluated from the same byte tables the kernels use, and
  * top16[i] = its top 16 bits as the prefilter tables give them. */

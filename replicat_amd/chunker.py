@@ -107,6 +107,20 @@ class GpuChunker:
         base = np.concatenate([[0], np.cumsum(caps)[:-1]]).astype(np.int64)
         return [cuts[b:b + c] for b, c in zip(base, counts)]
 
+    def tile_records(self, ptrs, lens, last_piece=None):
+        """(keys, js) of the per-tile phase over device streams (inspection / tests)."""
+        ptrs, lens = _ptr_array(ptrs), _ptr_array(lens)
+        last = _ptr_array(last_piece if last_piece is not None else np.zeros(len(lens)))
+        nt = ctypes.c_uint64()
+        check(lib().rc_tile_records(self._h, len(lens), ptrs.ctypes.data, lens.ctypes.data,
+                                    last.ctypes.data, None, None, 0, ctypes.byref(nt)))
+        keys = np.zeros(max(nt.value, 1), dtype=np.uint64)
+        js = np.zeros(max(nt.value, 1), dtype=np.uint64)
+        check(lib().rc_tile_records(self._h, len(lens), ptrs.ctypes.data, lens.ctypes.data,
+                                    last.ctypes.data, keys.ctypes.data, js.ctypes.data,
+                                    nt.value, ctypes.byref(nt)))
+        return keys[:nt.value], js[:nt.value]
+
     # ---------------------------------------------------------------------- profiling
 
     def timing(self, enable: bool):
@@ -116,6 +130,10 @@ class GpuChunker:
         a, b, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_uint64()
         check(lib().rc_timing_read(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(n)))
         return a.value, b.value, n.value
+
+
+def tile_keys():
+    return lib().rc_tile_keys()
 
 
 def keys_needed(max_length, L, P):

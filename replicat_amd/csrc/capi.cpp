@@ -259,8 +259,7 @@ int stage_descriptors(rc_chunker *ch, Workspace &ws, uint64_t n, const uint8_t *
 int upload_and_launch(rc_chunker *ch, Workspace &ws, const Plan &plan, ChainParams prm,
                       uint64_t *d_cuts, int64_t *d_counts, hipStream_t stream) {
     if (int rc = ws.d_desc.ensure(plan.bytes)) return rc;
-    if (int rc = ws.d_records.ensure(std::max<uint64_t>(plan.n_tiles, 1) * sizeof(TileRecord)))
-        return rc;
+    if (int rc = ws.d_records.ensure((plan.n_tiles + 1) * sizeof(TileRecord))) return rc;
     HIP_TRY(hipMemcpyAsync(ws.d_desc.p, ws.h_desc.p, plan.bytes, hipMemcpyHostToDevice, stream));
     const StreamDesc d = desc_view(ws.d_desc.p, plan.n);
     std::array<hipEvent_t, 3> ev{};
@@ -585,6 +584,37 @@ int rc_chunk_host(rc_chunker *ch, uint64_t n, const uint8_t *const *streams, con
     }
     if (int rc = finish(0)) return rc;
     if (int rc = finish(1)) return rc;
+    return RC_OK;
+}
+
+uint64_t rc_tile_keys(void) { return kTileKeys; }
+
+int rc_tile_records(rc_chunker *ch, uint64_t n, const uint8_t *const *d_streams,
+                    const uint64_t *lens, const uint64_t *last_piece, uint64_t *keys,
+                    uint64_t *js, uint64_t cap, uint64_t *n_tiles) {
+    if (!ch || !n_tiles) return fail(RC_ERR_ARGUMENT, "null argument");
+    if (int rc = validate_streams(n, d_streams, lens, last_piece, true)) return rc;
+    std::lock_guard<std::mutex> lock(ch->mu);
+    DeviceGuard g(ch->device);
+    Plan plan;
+    Workspace &ws = acquire_ws(ch);
+    if (int rc = stage_descriptors(ch, ws, n, d_streams, lens, last_piece, plan)) return rc;
+    if (int rc = ws.d_desc.ensure(plan.bytes)) return rc;
+    if (int rc = ws.d_records.ensure((plan.n_tiles + 1) * sizeof(TileRecord))) return rc;
+    HIP_TRY(hipMemcpy(ws.d_desc.p, ws.h_desc.p, plan.bytes, hipMemcpyHostToDevice));
+    if (rc_launch_tiles(ch->d_tables, desc_view(ws.d_desc.p, n), n, plan.n_tiles,
+                        static_cast<TileRecord *>(ws.d_records.p), nullptr))
+        return fail(RC_ERR_HIP, "%s", rc_launch_error());
+    HIP_TRY(hipDeviceSynchronize());
+    std::vector<TileRecord> h(plan.n_tiles);
+    if (plan.n_tiles)
+        HIP_TRY(hipMemcpy(h.data(), ws.d_records.p, plan.n_tiles * sizeof(TileRecord),
+                          hipMemcpyDeviceToHost));
+    *n_tiles = plan.n_tiles;
+    for (uint64_t t = 0; t < plan.n_tiles && t < cap; ++t) {
+        keys[t] = h[t].key;
+        js[t] = h[t].j;
+    }
     return RC_OK;
 }
 

@@ -15,8 +15,8 @@
 
 namespace rc {
 
-constexpr int kTileKeys = 4096;      // keys per tile = one wave: 64 lanes x 16 iters x 4 keys
-constexpr int kTileIters = 16;       // 16-byte loads per lane per tile
+constexpr int kTileIters = 16;       // 16-byte loads per lane per tile (16 KiB in flight per wave)
+constexpr int kTileKeys = 64 * 4 * kTileIters;  // keys per tile = one wave: 64 lanes x 4 keys
 constexpr int kWaveSize = 64;
 constexpr int kTileWaves = 16;       // waves per workgroup of the tile kernel (1024 threads)
 constexpr int kChainWaves = 4;       // waves (= streams) per workgroup of the chain kernel
@@ -75,6 +75,7 @@ __host__ __device__ inline uint64_t splitmix64(uint64_t x) {
 
 // Launchers implemented in kernels.hip (host-callable, enqueue only).
 extern "C" {
+// d_records: n_tiles + 1 entries (the last is scratch for the tile kernel's pipeline)
 int rc_launch_tiles(const rc::KeyTables *d_tables, rc::StreamDesc desc, uint64_t n_streams,
                     uint64_t n_tiles, rc::TileRecord *d_records, void *stream);
 int rc_launch_chain(const rc::KeyTables *d_tables, rc::StreamDesc desc, uint64_t n_streams,

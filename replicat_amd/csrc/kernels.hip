@@ -4,7 +4,7 @@
 // with two launches per batch of streams:
 //
 //   phase A  tile kernel   (HBM-bound, one pass over every input byte)
-//            Every wave owns 4096-key tiles (16 KiB of stream) and reduces each to one
+//            Every wave owns 2048-key tiles (8 KiB of stream) and reduces each to one
 //            TileRecord = (first maximal 64-bit key, its index).  Bytes stream straight from
 //            HBM into registers with coalesced 16-byte loads (1 KiB per wave instruction).
 //            Per key it evaluates only the top 16 bits of the hash: 4 conflict-free LDS
@@ -33,12 +33,42 @@ namespace {
 thread_local char g_launch_err[256];
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// Stream bytes are global memory; the pointers come out of descriptor arrays, so say so
+// explicitly -- a flat (generic) load also counts against lgkmcnt and would make every LDS
+// wait drain the whole in-flight HBM stream.
+typedef __attribute__((address_space(1))) const u32x4 gu32x4;
+typedef __attribute__((address_space(1))) const uint32_t gu32;
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63; }
 
-__device__ __forceinline__ uint32_t ld_u32(const uint8_t *p) {
-    return *reinterpret_cast<const uint32_t *>(p);
+// v_max3_u32 as an opaque step: left to itself LLVM reassociates the running maxima of the
+// unrolled tile loop into one tree at the end, keeping every intermediate alive (spills).
+__device__ __forceinline__ uint32_t max3_u32(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_max3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
 }
+
+
+// Lane l's 64-bit value (readlane returns int: keep both halves unsigned).
+__device__ __forceinline__ uint64_t lane_u64(uint64_t v, int l) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((uint32_t)v, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Descriptor words through the SCALAR cache (constant address space -> s_load): a vector load
+// would sit in the in-order vmcnt queue behind the stream prefetch and its wait would drain it.
+typedef __attribute__((address_space(4))) const uint64_t cu64;
+__device__ __forceinline__ uint64_t sload(const uint64_t *p) { return *(cu64 *)(p); }
+__device__ __forceinline__ const uint8_t *sload_ptr(const uint8_t *const *p) {
+    return reinterpret_cast<const uint8_t *>(sload(reinterpret_cast<const uint64_t *>(p)));
+}
+
+__device__ __forceinline__ uint32_t ld_u32(const uint8_t *p) {
+    return *(gu32 *)(p);
+}
+__device__ __forceinline__ gu32x4 *as_global_x4(const uint8_t *p) { return (gu32x4 *)(p); }
 
 // Exact 64-bit key of (w[j-1], w[j]) from the byte tables (gclmul.h), k1 included.
 __device__ __forceinline__ uint64_t full_key(const uint64_t *__restrict__ tl,
@@ -47,12 +77,6 @@ __device__ __forceinline__ uint64_t full_key(const uint64_t *__restrict__ tl,
     return tl[wlo & 255] ^ tl[256 + ((wlo >> 8) & 255)] ^ tl[512 + ((wlo >> 16) & 255)] ^
            tl[768 + (wlo >> 24)] ^ th[whi & 255] ^ th[256 + ((whi >> 8) & 255)] ^
            th[512 + ((whi >> 16) & 255)] ^ th[768 + (whi >> 24)];
-}
-
-__device__ __forceinline__ uint64_t key_at(const uint64_t *tl, const uint64_t *th,
-                                           const uint8_t *base, uint64_t j) {
-    const uint8_t *p = base + 4 * j;
-    return full_key(tl, th, ld_u32(p - 4), ld_u32(p));
 }
 
 // (key desc, index asc) maximum over the wave; every lane gets the result.
@@ -77,6 +101,16 @@ __device__ __forceinline__ uint32_t pf_lds(uint32_t byte_addr) {
                                                byte_addr);
 }
 
+__device__ __forceinline__ void pf_addrs(uint32_t w, uint32_t lb_a, uint32_t lb_b, uint32_t *a) {
+    a[0] = __builtin_amdgcn_perm(w, lb_a, 0x0c020400u);
+    a[1] = __builtin_amdgcn_perm(w, lb_a, 0x0c020500u) + 128;
+    a[2] = __builtin_amdgcn_perm(w, lb_b, 0x0c020600u);
+    a[3] = __builtin_amdgcn_perm(w, lb_b, 0x0c020700u) + 128;
+}
+__device__ __forceinline__ uint32_t pf_gather(const uint32_t *a) {
+    return pf_lds(a[0]) ^ pf_lds(a[1]) ^ pf_lds(a[2]) ^ pf_lds(a[3]);
+}
+
 // 32-bit prefilter entry of a word: top16(Lmap(w)) << 16 | top16(Hmap(w)).
 // v_perm builds each table address (v << 8 | lane's bank column | table half) in one op.
 __device__ __forceinline__ uint32_t pf_entry(uint32_t w, uint32_t lb_a, uint32_t lb_b) {
@@ -87,43 +121,96 @@ __device__ __forceinline__ uint32_t pf_entry(uint32_t w, uint32_t lb_a, uint32_t
     return pf_lds(a0) ^ pf_lds(a1 + 128) ^ pf_lds(a2) ^ pf_lds(a3 + 128);
 }
 
-// Exact per-key path over keys [ja, jb] of the tile starting at key j0 (edge tiles, tie
-// fallback, unaligned streams).  Same key -> lane mapping as the fast path.
-__device__ void tile_exact(const uint64_t *tl, const uint64_t *th, const uint8_t *base,
-                           uint64_t j0, uint64_t ja, uint64_t jb, uint64_t &bk, uint64_t &bj) {
-    const uint32_t lane = lane_id();
-    bk = 0;
-    bj = ~0ull;
-    for (int m = 0; m < 64; ++m) {
-        const uint64_t j = j0 + (uint64_t)(m >> 2) * 256 + lane * 4 + (m & 3);
-        if (j >= ja && j <= jb) {
-            const uint64_t k = key_at(tl, th, base, j);
-            if (k > bk) {
-                bk = k;
-                bj = j;
-            }
-        }
+// (key desc, index asc) improvement test: the lexicographic order makes the merge of ranges
+// and records independent of the order in which a lane visits them.
+__device__ __forceinline__ void take_best(uint64_t k, uint64_t j, uint64_t &bk, uint64_t &bj) {
+    if (k > bk || (k == bk && j < bj)) {
+        bk = k;
+        bj = j;
     }
-    wave_best(bk, bj);
 }
 
-__device__ __forceinline__ void tile_fast(const uint64_t *tl, const uint64_t *th,
-                                          const uint8_t *base, uint64_t j0, uint32_t lb_a,
-                                          uint32_t lb_b, uint64_t &bk, uint64_t &bj) {
-    const uint32_t lane = lane_id();
-    const u32x4 *src = reinterpret_cast<const u32x4 *>(base + 4 * j0);
-    u32x4 x[kTileIters];
-#pragma unroll
-    for (int it = 0; it < kTileIters; ++it) x[it] = __builtin_nontemporal_load(src + it * 64 + lane);
+// Best exact key over the two key ranges [a0, b0] and [a1, b1] of one stream (either may be
+// empty: a > b).  Lanes take consecutive keys (coalesced 256-B loads); every round first
+// issues all kChainUnroll x 2 x 2 word loads of the lane, then evaluates, so one round costs
+// one memory latency instead of one per key.
+constexpr int kChainUnroll = 16;
 
-    uint32_t carry = pf_entry(ld_u32(base + 4 * j0 - 4), lb_a, lb_b);
+__device__ __forceinline__ void scan_ranges(const uint64_t *tl, const uint64_t *th,
+                                            const uint8_t *base, uint64_t a0, uint64_t b0,
+                                            uint64_t a1, uint64_t b1, uint64_t &bk,
+                                            uint64_t &bj) {
+    const uint64_t lane = lane_id();
+    for (uint64_t r = 0;; r += 64 * kChainUnroll) {
+        const bool live0 = a0 <= b0 && a0 + r <= b0, live1 = a1 <= b1 && a1 + r <= b1;
+        if (!live0 && !live1) break;
+        uint32_t lo0[kChainUnroll], hi0[kChainUnroll], lo1[kChainUnroll], hi1[kChainUnroll];
+#pragma unroll
+        for (int u = 0; u < kChainUnroll; ++u) {
+            const uint64_t j0 = a0 + r + 64 * u + lane, j1 = a1 + r + 64 * u + lane;
+            if (live0 && j0 <= b0) {
+                lo0[u] = ld_u32(base + 4 * j0 - 4);
+                hi0[u] = ld_u32(base + 4 * j0);
+            }
+            if (live1 && j1 <= b1) {
+                lo1[u] = ld_u32(base + 4 * j1 - 4);
+                hi1[u] = ld_u32(base + 4 * j1);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kChainUnroll; ++u) {
+            const uint64_t j0 = a0 + r + 64 * u + lane, j1 = a1 + r + 64 * u + lane;
+            if (live0 && j0 <= b0) take_best(full_key(tl, th, lo0[u], hi0[u]), j0, bk, bj);
+            if (live1 && j1 <= b1) take_best(full_key(tl, th, lo1[u], hi1[u]), j1, bk, bj);
+        }
+    }
+}
+
+// Where a wave's tile lives.  `fast` = a full interior tile (keys j0 .. j0+4095 all needed,
+// j0 >= kTileKeys); tile 0 and a partial last tile of every stream go to the edge kernel.
+struct TileRef {
+    const uint8_t *base;
+    uint64_t j0;
+    bool fast;
+};
+
+constexpr uint32_t kLastLocal = 4 * kTileIters - 1;
+constexpr uint64_t kTieMark = ~0ull;  // TileRecord.j of a tile left to the exact path  // a lane's keys in a tile: 0 .. kLastLocal
+
+// Fast path over a tile whose kTileIters loads are in flight in x[].  As iteration `it` consumes
+// x[it] it re-issues x[it] for the wave's NEXT fast tile (if any), so every wave keeps
+// 8 KiB of HBM reads in flight through its compute phase (a register ring: no extra VGPRs,
+// the in-order vmcnt does the bookkeeping).
+//
+// Returns the lane's largest top-16 value and the first and last local index where it occurs.
+// `prev_word` holds the word before the tile (key j0's low half) and is refilled with the next
+// tile's, issued with the ring.
+__device__ __forceinline__ void tile_scan(const TileRef &tr, const TileRef &nx,
+                                          u32x4 (&x)[kTileIters], uint32_t &prev_word,
+                                          uint32_t lb_a, uint32_t lb_b, uint32_t &top,
+                                          uint32_t &first, uint32_t &last) {
+    const uint32_t lane = lane_id();
+    // no next fast tile (end of the wave's range): harmlessly re-read this tile instead, so
+    // the ring loads stay unconditional
+    const uint8_t *nbase = nx.fast ? nx.base + 4 * nx.j0 : tr.base + 4 * tr.j0;
+    gu32x4 *nsrc = as_global_x4(nbase) + lane;
+    uint32_t carry = pf_entry(prev_word, lb_a, lb_b);
+    prev_word = ld_u32(nbase - 4);
     uint32_t acc_first = 0, acc_last = 0;
 #pragma unroll
     for (int it = 0; it < kTileIters; ++it) {
-        const uint32_t e0 = pf_entry(x[it].x, lb_a, lb_b);
-        const uint32_t e1 = pf_entry(x[it].y, lb_a, lb_b);
-        const uint32_t e2 = pf_entry(x[it].z, lb_a, lb_b);
-        const uint32_t e3 = pf_entry(x[it].w, lb_a, lb_b);
+        // the 16 table addresses of this 16-byte slice; then the slot is free for the next
+        // tile's slice (same registers: no copies when the loop wraps)
+        uint32_t a[16];
+        pf_addrs(x[it].x, lb_a, lb_b, a + 0);
+        pf_addrs(x[it].y, lb_a, lb_b, a + 4);
+        pf_addrs(x[it].z, lb_a, lb_b, a + 8);
+        pf_addrs(x[it].w, lb_a, lb_b, a + 12);
+        x[it] = __builtin_nontemporal_load(nsrc + it * 64);
+        const uint32_t e0 = pf_gather(a + 0);
+        const uint32_t e1 = pf_gather(a + 4);
+        const uint32_t e2 = pf_gather(a + 8);
+        const uint32_t e3 = pf_gather(a + 12);
         // previous word's entry for key 0 of this lane: lane-1's e3 (wave_ror:1); lane 0 takes
         // the carry = lane 63's e3 of the previous iteration (or the word before the tile).
         const uint32_t rot = __builtin_amdgcn_update_dpp(0u, e3, 0x13C, 0xf, 0xf, false);
@@ -133,29 +220,63 @@ __device__ __forceinline__ void tile_fast(const uint64_t *tl, const uint64_t *th
         const uint32_t b1 = (e0 & 0xffff0000u) ^ (e1 << 16);
         const uint32_t b2 = (e1 & 0xffff0000u) ^ (e2 << 16);
         const uint32_t b3 = (e2 & 0xffff0000u) ^ (e3 << 16);
-        // local key index l = 4*it + k;  "first" packs 63 - l, "last" packs l
-        const uint32_t inv = 60u - 4u * it, idx = 4u * it;
-        acc_first = max(acc_first, max(b0 | inv | 3u, b1 | inv | 2u));
-        acc_first = max(acc_first, max(b2 | inv | 1u, b3 | inv));
-        acc_last = max(acc_last, max(b0 | idx, b1 | idx | 1u));
-        acc_last = max(acc_last, max(b2 | idx | 2u, b3 | idx | 3u));
+        // local key index l = 4*it + k;  "first" packs kLastLocal - l, "last" packs l
+        const uint32_t inv = kLastLocal - 3u - 4u * it, idx = 4u * it;
+        acc_first = max3_u32(acc_first, b0 | inv | 3u, b1 | inv | 2u);
+        acc_first = max3_u32(acc_first, b2 | inv | 1u, b3 | inv);
+        acc_last = max3_u32(acc_last, b0 | idx, b1 | idx | 1u);
+        acc_last = max3_u32(acc_last, b2 | idx | 2u, b3 | idx | 3u);
     }
-    const uint32_t top = acc_first >> 16;
-    const uint32_t first = 63u - (acc_first & 0xffffu);
-    const uint32_t last = acc_last & 0xffffu;
-    const uint64_t j = j0 + (uint64_t)(first >> 2) * 256 + lane * 4 + (first & 3);
-    bk = key_at(tl, th, base, j);
-    bj = j;
-    wave_best(bk, bj);
-    const bool tie = top == (uint32_t)(bk >> 48) && first != last;
-    if (__any(tie)) tile_exact(tl, th, base, j0, j0, j0 + kTileKeys - 1, bk, bj);
+    top = acc_first >> 16;
+    first = kLastLocal - (acc_first & 0xffffu);
+    last = acc_last & 0xffffu;
 }
 
-__global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restrict__ tab,
-                                                       StreamDesc d, uint64_t n_streams,
-                                                       uint64_t n_tiles,
-                                                       TileRecord *__restrict__ rec) {
-    // stage the replicated prefilter tables and the exact tables into LDS
+// Maximum over the wave, returned in SGPRs: DPP shifts within each 16-lane row, then the
+// four row maxima (lanes 15, 31, 47, 63) through readlane.
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false));
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false));
+    const uint32_t r0 = __builtin_amdgcn_readlane(v, 15), r1 = __builtin_amdgcn_readlane(v, 31);
+    const uint32_t r2 = __builtin_amdgcn_readlane(v, 47), r3 = __builtin_amdgcn_readlane(v, 63);
+    return max(max(r0, r1), max(r2, r3));
+}
+
+// Walks a wave's tile range across stream boundaries (all state wave-uniform).
+struct TileCursor {
+    StreamDesc d;
+    uint64_t s, cur, next;
+    __device__ void init(const StreamDesc &dd, uint64_t n_streams, uint64_t t) {
+        d = dd;
+        uint64_t lo = 0, hi = n_streams;  // largest s with tile_base[s] <= t
+        while (hi - lo > 1) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (sload(d.tile_base + mid) <= t) lo = mid;
+            else hi = mid;
+        }
+        s = lo;
+        cur = sload(d.tile_base + s);
+        next = sload(d.tile_base + s + 1);
+    }
+    __device__ TileRef at(uint64_t t) {  // t must not decrease between calls
+        while (t >= next) {
+            ++s;
+            cur = next;
+            next = sload(d.tile_base + s + 1);
+        }
+        TileRef r;
+        r.base = sload_ptr(d.ptr + s);
+        r.j0 = (t - cur) * kTileKeys;
+        r.fast = __builtin_amdgcn_readfirstlane(
+                     (uint32_t)(r.j0 >= kTileKeys && r.j0 + kTileKeys - 1 <= sload(d.jneed + s))) != 0;
+        return r;
+    }
+};
+
+__device__ __forceinline__ void stage_tile_tables(const KeyTables *tab) {
+    // the 32x replicated prefilter tables and the exact tables
     for (uint32_t i = threadIdx.x; i < 1024u * 32u; i += blockDim.x) {
         const uint32_t e = i >> 5, c = i & 31, b = e >> 8, v = e & 255;
         s_tile_lds[((b >> 1) * 65536u + v * 256u + (b & 1) * 128u) / 4 + c] = tab->pf[b][v];
@@ -164,6 +285,15 @@ __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restri
     const uint64_t *gfull = &tab->tl[0][0];
     for (uint32_t i = threadIdx.x; i < 2048u; i += blockDim.x) full[i] = gfull[i];
     __syncthreads();
+}
+
+// Persistent: one 1024-thread workgroup per CU, each wave a contiguous range of tiles.
+__global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restrict__ tab,
+                                                       StreamDesc d, uint64_t n_streams,
+                                                       uint64_t n_tiles,
+                                                       TileRecord *__restrict__ rec) {
+    stage_tile_tables(tab);
+    const uint64_t *full = reinterpret_cast<const uint64_t *>(s_tile_lds + kFullOff / 4);
     const uint64_t *tl = full, *th = full + 1024;
 
     const uint32_t lane = lane_id();
@@ -175,53 +305,166 @@ __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restri
     const uint64_t t_end = n_tiles * (gw + 1) / nw;
     if (t >= t_end) return;
 
-    // stream of tile t: largest s with tile_base[s] <= t
+    TileCursor cursor;
+    cursor.init(d, n_streams, t);
+    TileRef cur = cursor.at(t);
+    while (!cur.fast && ++t < t_end) cur = cursor.at(t);
+    if (!cur.fast) return;
+    u32x4 x[kTileIters];
+    uint32_t prev_word = ld_u32(cur.base + 4 * cur.j0 - 4);
+    {
+        gu32x4 *src = as_global_x4(cur.base + 4 * cur.j0) + lane;
+#pragma unroll
+        for (int it = 0; it < kTileIters; ++it) {
+            x[it] = __builtin_nontemporal_load(src + it * 64);
+            __builtin_amdgcn_sched_barrier(0);  // issue in ring order: the waits count on it
+        }
+    }
+    // Records are produced one tile late: a tile's candidate words are loaded when it ends and
+    // its exact key is evaluated (and its record stored) at the end of the next tile, when the
+    // load has long landed.  Every tile issues the same vector-memory sequence (ring loads,
+    // neighbour word, candidate words, one record store) so the compiler's in-order vmcnt
+    // waits stay exact; the first store goes to the spare record at n_tiles.
+    uint64_t pend_t = n_tiles, pend_j0 = 0;  // SGPRs: the pending tile and its first key
+    uint64_t pend_mask = 0;                   // candidate lanes (0 = marker record)
+    uint32_t pend_lo = 0, pend_hi = 0, pend_jl = 0;  // per lane: candidate words and index
+
+    for (;;) {
+        TileRef nx = cur;
+        nx.fast = false;
+        uint64_t tn = t + 1;
+        for (; tn < t_end; ++tn) {
+            nx = cursor.at(tn);
+            if (nx.fast) break;
+        }
+        uint32_t top, first, last;
+        tile_scan(cur, nx, x, prev_word, lb_a, lb_b, top, first, last);
+
+        // retire the pending tile: (first maximal exact key, index) over its candidate lanes
+        {
+            const uint64_t k = full_key(tl, th, pend_lo, pend_hi);
+            uint64_t bk = 0, bj = kTieMark;
+            for (uint64_t m = pend_mask; m; m &= m - 1) {  // usually one lane
+                const int l = __builtin_ctzll(m);
+                const uint64_t kl = lane_u64(k, l);
+                const uint64_t jl = pend_j0 + (uint32_t)__builtin_amdgcn_readlane(pend_jl, l);
+                if (bj == kTieMark || kl > bk || (kl == bk && jl < bj)) {
+                    bk = kl;
+                    bj = jl;
+                }
+            }
+            if (lane == 0) {
+                rec[pend_t].key = bk;
+                rec[pend_t].j = bj;
+            }
+        }
+
+        // this tile: largest top-16 value, then the lowest tile-local index holding it; the
+        // lanes holding that value are the candidates.  A candidate lane whose maximum occurs
+        // twice cannot name its first maximal key: the tile becomes a marker record and the
+        // edge kernel recomputes it exactly.
+        const uint32_t jl = (first >> 2) * 256 + lane * 4 + (first & 3);
+        const uint32_t p = wave_max_u32((top << 16) | (0xffffu - jl));
+        const bool cand = top == (p >> 16);
+        const uint64_t cmask = __ballot(cand);
+        const bool tie = __any(cand && first != last);
+        const uint32_t win = 0xffffu - (p & 0xffffu);
+        pend_t = t;
+        pend_j0 = cur.j0;
+        pend_mask = tie ? 0 : cmask;
+        pend_jl = cand ? jl : win;  // non-candidates load the winner's (same) line
+        const uint8_t *q = cur.base + 4 * (cur.j0 + pend_jl);
+        pend_lo = ld_u32(q - 4);
+        pend_hi = ld_u32(q);
+
+        if (!nx.fast) break;
+        t = tn;
+        cur = nx;
+    }
+    {
+        const uint64_t k = full_key(tl, th, pend_lo, pend_hi);
+        uint64_t bk = 0, bj = kTieMark;
+        for (uint64_t m = pend_mask; m; m &= m - 1) {
+            const int l = __builtin_ctzll(m);
+            const uint64_t kl = lane_u64(k, l);
+            const uint64_t jl = pend_j0 + (uint32_t)__builtin_amdgcn_readlane(pend_jl, l);
+            if (bj == kTieMark || kl > bk || (kl == bk && jl < bj)) {
+                bk = kl;
+                bj = jl;
+            }
+        }
+        if (lane == 0) {
+            rec[pend_t].key = bk;
+            rec[pend_t].j = bj;
+        }
+    }
+}
+
+__device__ __forceinline__ uint64_t stream_of_tile(const StreamDesc &d, uint64_t n_streams,
+                                                   uint64_t t) {
     uint64_t lo = 0, hi = n_streams;
     while (hi - lo > 1) {
         const uint64_t mid = (lo + hi) >> 1;
-        if (d.tile_base[mid] <= t) lo = mid;
+        if (sload(d.tile_base + mid) <= t) lo = mid;
         else hi = mid;
     }
-    uint64_t s = lo, cur = d.tile_base[s], next = d.tile_base[s + 1];
-    for (; t < t_end; ++t) {
-        while (t >= next) {
-            ++s;
-            cur = next;
-            next = d.tile_base[s + 1];
-        }
-        const uint8_t *base = d.ptr[s];
-        const uint64_t jneed = d.jneed[s];
-        const uint64_t j0 = (t - cur) * kTileKeys;
-        uint64_t bk, bj;
-        const bool fast = j0 >= kTileKeys && j0 + kTileKeys - 1 <= jneed &&
-                          (reinterpret_cast<uintptr_t>(base) & 15) == 0;
-        if (fast) {
-            tile_fast(tl, th, base, j0, lb_a, lb_b, bk, bj);
+    return lo;
+}
+
+__device__ __forceinline__ void exact_tile(const uint64_t *tl, const uint64_t *th,
+                                           const StreamDesc &d, uint64_t s, uint64_t t,
+                                           TileRecord *rec) {
+    const uint64_t j0 = (t - sload(d.tile_base + s)) * kTileKeys;
+    const uint64_t jb = min(j0 + kTileKeys - 1, sload(d.jneed + s));
+    uint64_t bk = 0, bj = ~0ull;
+    scan_ranges(tl, th, sload_ptr(d.ptr + s), max(j0, (uint64_t)1), jb, 1, 0, bk, bj);
+    wave_best(bk, bj);
+    if (lane_id() == 0) {
+        rec[t].key = bk;
+        rec[t].j = bj;
+    }
+}
+
+// Exact tiles, one wave per item, grid-strided: items 0 .. 2n-1 are tile 0 and a partial
+// last tile of every stream; the rest sweep the records in 64-record chunks for the tiles the
+// fast kernel marked (kTieMark) and recompute those.
+__global__ __launch_bounds__(256) void rc_edge_kernel(const KeyTables *__restrict__ tab,
+                                                      StreamDesc d, uint64_t n_streams,
+                                                      uint64_t n_tiles,
+                                                      TileRecord *__restrict__ rec) {
+    __shared__ __attribute__((aligned(16))) uint64_t s_full[2048];
+    const uint64_t *gfull = &tab->tl[0][0];
+    for (uint32_t i = threadIdx.x; i < 2048u; i += blockDim.x) s_full[i] = gfull[i];
+    __syncthreads();
+    const uint64_t *tl = s_full, *th = s_full + 1024;
+    const uint64_t gw = (uint64_t)blockIdx.x * (blockDim.x >> 6) +
+                        __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    const uint64_t n_chunks = (n_tiles + 63) / 64;
+    for (uint64_t e = gw; e < 2 * n_streams + n_chunks; e += nw) {
+        if (e < 2 * n_streams) {
+            const uint64_t s = e >> 1;
+            const uint64_t tb = sload(d.tile_base + s), nt = sload(d.tile_base + s + 1) - tb;
+            if (nt == 0) continue;
+            uint64_t t = tb;
+            if (e & 1) {  // the last tile, unless it is tile 0 or a full (fast) tile
+                if (nt < 2) continue;
+                if ((nt - 1) * kTileKeys + kTileKeys - 1 <= sload(d.jneed + s)) continue;
+                t = tb + nt - 1;
+            }
+            exact_tile(tl, th, d, s, t, rec);
         } else {
-            const uint64_t jb = min(j0 + kTileKeys - 1, jneed);
-            tile_exact(tl, th, base, j0, max(j0, (uint64_t)1), jb, bk, bj);
-        }
-        if (lane == 0) {
-            rec[t].key = bk;
-            rec[t].j = bj;
+            const uint64_t t0 = (e - 2 * n_streams) * 64, t = t0 + lane_id();
+            const bool marked = t < n_tiles && rec[t].j == kTieMark;
+            for (uint64_t m = __ballot(marked); m; m &= m - 1) {
+                const uint64_t tm = t0 + __builtin_ctzll(m);
+                exact_tile(tl, th, d, stream_of_tile(d, n_streams, tm), tm, rec);
+            }
         }
     }
 }
 
 // ----------------------------------------------------------------- phase B: chain kernel
-
-// best (key desc, index asc) over the exact keys [a, b] of one stream, lanes strided
-__device__ __forceinline__ void scan_exact(const uint64_t *tl, const uint64_t *th,
-                                           const uint8_t *base, uint64_t a, uint64_t b,
-                                           uint64_t &bk, uint64_t &bj) {
-    for (uint64_t j = a + lane_id(); j <= b; j += 64) {
-        const uint64_t k = key_at(tl, th, base, j);
-        if (k > bk) {
-            bk = k;
-            bj = j;
-        }
-    }
-}
 
 __global__ __launch_bounds__(256) void rc_chain_kernel(const KeyTables *__restrict__ tab,
                                                        StreamDesc d, uint64_t n_streams,
@@ -273,17 +516,14 @@ __global__ __launch_bounds__(256) void rc_chain_kernel(const KeyTables *__restri
                 const uint64_t t_lo = (ja + kTileKeys - 1) / kTileKeys;
                 const uint64_t t_hi = (jb + 1) / kTileKeys;
                 if (t_lo < t_hi) {
-                    scan_exact(tl, th, base, ja, t_lo * kTileKeys - 1, bk, bj);
                     for (uint64_t t = t_lo + lane; t < t_hi; t += 64) {
                         const TileRecord r = rec[tb0 + t];
-                        if (r.key > bk) {
-                            bk = r.key;
-                            bj = r.j;
-                        }
+                        if (r.key != 0) take_best(r.key, r.j, bk, bj);
                     }
-                    scan_exact(tl, th, base, t_hi * kTileKeys, jb, bk, bj);
+                    scan_ranges(tl, th, base, ja, t_lo * kTileKeys - 1, t_hi * kTileKeys, jb,
+                                bk, bj);
                 } else {
-                    scan_exact(tl, th, base, ja, jb, bk, bj);
+                    scan_ranges(tl, th, base, ja, jb, 1, 0, bk, bj);
                 }
                 wave_best(bk, bj);
             }
@@ -352,13 +592,21 @@ const char *rc_launch_error(void) { return g_launch_err; }
 int rc_launch_tiles(const KeyTables *d_tables, StreamDesc desc, uint64_t n_streams,
                     uint64_t n_tiles, TileRecord *d_records, void *stream) {
     if (n_tiles == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
     const uint64_t waves_per_wg = 1024 / kWaveSize;
     uint64_t grid = (n_tiles + waves_per_wg - 1) / waves_per_wg;
     const uint64_t cus = (uint64_t)cu_count();
     if (grid > cus) grid = cus;  // persistent: one 144 KiB-LDS workgroup per CU
-    hipLaunchKernelGGL(rc_tile_kernel, dim3((unsigned)grid), dim3(1024), 0,
-                       (hipStream_t)stream, d_tables, desc, n_streams, n_tiles, d_records);
-    return launch_status("rc_tile_kernel");
+    hipLaunchKernelGGL(rc_tile_kernel, dim3((unsigned)grid), dim3(1024), 0, st, d_tables, desc,
+                       n_streams, n_tiles, d_records);
+    if (launch_status("rc_tile_kernel")) return 1;
+    // edge tiles (2 per stream) + the marked-tile sweep (64 records per item), one wave each
+    uint64_t egrid = (2 * n_streams + (n_tiles + 63) / 64 + 3) / 4;
+    if (egrid > 4 * cus) egrid = 4 * cus;
+    if (egrid == 0) egrid = 1;
+    hipLaunchKernelGGL(rc_edge_kernel, dim3((unsigned)egrid), dim3(256), 0, st, d_tables, desc,
+                       n_streams, n_tiles, d_records);
+    return launch_status("rc_edge_kernel");
 }
 
 int rc_launch_chain(const KeyTables *d_tables, StreamDesc desc, uint64_t n_streams,

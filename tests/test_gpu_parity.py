@@ -230,3 +230,41 @@ def test_host_path_matches_device():
     got = ch.chunk_host(bufs)
     for b, g in zip(bufs, got):
         assert g.tolist() == o.chunk_stream(b, 128_000, 5_120_000, None, 0)
+
+
+@pytest.mark.parametrize('kind', ['random', 'zeros', 'periodic', 'seeded_key'])
+def test_tile_records_vs_oracle(kind):
+    """Phase A alone: every tile record (first maximal exact key, index) equals the oracle's."""
+    import ctypes
+    o = _oracle()
+    from replicat_amd.chunker import keys_needed, tile_keys
+    tk = tile_keys()
+    key = synth.seeded_key(9) if kind == 'seeded_key' else b'\xff' * 16
+    mn, mx = 128_000, 5_120_000
+    ch = GpuChunker(mn, mx, key)
+    sizes = [(16 << 20) + 4 * 777, 12 << 20, 5 << 20]
+    rnd = np.random.default_rng(3)
+    if kind == 'zeros':
+        datas = [np.zeros(n, np.uint8) for n in sizes]
+    elif kind == 'periodic':
+        datas = [np.resize(rnd.integers(0, 256, 4096 + 12, dtype=np.uint8), n) for n in sizes]
+    else:
+        datas = [synth.stream_bytes(n, synth.DEFAULT_SEED, 100 + i) for i, n in enumerate(sizes)]
+    ts = device_streams(sizes, datas=datas)
+    keys, js = ch.tile_records([t.data_ptr() for t in ts], sizes, [0] * len(sizes))
+    k0 = int.from_bytes(key[:8], 'little')
+    k1 = int.from_bytes(key[8:], 'little')
+    base = 0
+    for d, n in zip(datas, sizes):
+        jneed = keys_needed(mx, n, 0)
+        nt = jneed // tk + 1 if jneed else 0
+        ek = np.zeros(max(nt, 1), np.uint64)
+        ej = np.zeros(max(nt, 1), np.uint64)
+        buf = np.concatenate([d, np.zeros(16, np.uint8)])
+        o.lib().oc_tile_records(k0, k1, buf.ctypes.data, jneed, tk, nt, ek.ctypes.data,
+                                ej.ctypes.data)
+        gk, gj = keys[base:base + nt], js[base:base + nt]
+        bad = np.nonzero((gk != ek[:nt]) | ((gj != ej[:nt]) & (ek[:nt] != 0)))[0]
+        assert bad.size == 0, (kind, n, bad[:8].tolist(), gk[bad[:4]].tolist(), ek[bad[:4]].tolist(),
+                               gj[bad[:4]].tolist(), ej[bad[:4]].tolist())
+        base += nt
