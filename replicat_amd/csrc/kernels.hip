@@ -131,38 +131,56 @@ __device__ __forceinline__ void take_best(uint64_t k, uint64_t j, uint64_t &bk, 
 }
 
 // Best exact key over the two key ranges [a0, b0] and [a1, b1] of one stream (either may be
-// empty: a > b).  Lanes take consecutive keys (coalesced 256-B loads); every round first
-// issues all kChainUnroll x 2 x 2 word loads of the lane, then evaluates, so one round costs
-// one memory latency instead of one per key.
-constexpr int kChainUnroll = 16;
+// empty: a > b).  Lanes take consecutive keys (coalesced 256-B loads).  Every round first
+// issues all of the lane's loads -- unconditionally, at indices clamped into the range, so
+// the compiler cannot serialise them behind divergent branches -- then evaluates, so a round
+// costs one memory latency.
+constexpr int kScanUnroll = 32;
 
 __device__ __forceinline__ void scan_ranges(const uint64_t *tl, const uint64_t *th,
                                             const uint8_t *base, uint64_t a0, uint64_t b0,
                                             uint64_t a1, uint64_t b1, uint64_t &bk,
                                             uint64_t &bj) {
+    const bool e0 = a0 <= b0, e1 = a1 <= b1;
+    if (!e0 && !e1) return;
+    if (!e0) a0 = b0 = a1;  // a valid dummy key, never taken
+    if (!e1) a1 = b1 = a0;
     const uint64_t lane = lane_id();
-    for (uint64_t r = 0;; r += 64 * kChainUnroll) {
-        const bool live0 = a0 <= b0 && a0 + r <= b0, live1 = a1 <= b1 && a1 + r <= b1;
+    for (uint64_t r = 0;; r += 64 * kScanUnroll) {
+        const bool live0 = e0 && a0 + r <= b0, live1 = e1 && a1 + r <= b1;
         if (!live0 && !live1) break;
-        uint32_t lo0[kChainUnroll], hi0[kChainUnroll], lo1[kChainUnroll], hi1[kChainUnroll];
+        uint2 w0[kScanUnroll], w1[kScanUnroll];
 #pragma unroll
-        for (int u = 0; u < kChainUnroll; ++u) {
-            const uint64_t j0 = a0 + r + 64 * u + lane, j1 = a1 + r + 64 * u + lane;
-            if (live0 && j0 <= b0) {
-                lo0[u] = ld_u32(base + 4 * j0 - 4);
-                hi0[u] = ld_u32(base + 4 * j0);
-            }
-            if (live1 && j1 <= b1) {
-                lo1[u] = ld_u32(base + 4 * j1 - 4);
-                hi1[u] = ld_u32(base + 4 * j1);
-            }
+        for (int u = 0; u < kScanUnroll; ++u) {
+            const uint64_t j0 = min(a0 + r + 64 * u + lane, b0);
+            const uint64_t j1 = min(a1 + r + 64 * u + lane, b1);
+            w0[u].x = ld_u32(base + 4 * j0 - 4);
+            w0[u].y = ld_u32(base + 4 * j0);
+            w1[u].x = ld_u32(base + 4 * j1 - 4);
+            w1[u].y = ld_u32(base + 4 * j1);
         }
 #pragma unroll
-        for (int u = 0; u < kChainUnroll; ++u) {
+        for (int u = 0; u < kScanUnroll; ++u) {
             const uint64_t j0 = a0 + r + 64 * u + lane, j1 = a1 + r + 64 * u + lane;
-            if (live0 && j0 <= b0) take_best(full_key(tl, th, lo0[u], hi0[u]), j0, bk, bj);
-            if (live1 && j1 <= b1) take_best(full_key(tl, th, lo1[u], hi1[u]), j1, bk, bj);
+            if (e0 && j0 <= b0) take_best(full_key(tl, th, w0[u].x, w0[u].y), j0, bk, bj);
+            if (e1 && j1 <= b1) take_best(full_key(tl, th, w1[u].x, w1[u].y), j1, bk, bj);
         }
+    }
+}
+
+// Best record over tiles [t_lo, t_hi) of one stream, loads issued up front per round.
+constexpr int kRecUnroll = 8;
+
+__device__ __forceinline__ void scan_records(const TileRecord *rec, uint64_t t_lo, uint64_t t_hi,
+                                             uint64_t &bk, uint64_t &bj) {
+    const uint64_t lane = lane_id();
+    for (uint64_t r = t_lo; r < t_hi; r += 64 * kRecUnroll) {
+        TileRecord v[kRecUnroll];
+#pragma unroll
+        for (int u = 0; u < kRecUnroll; ++u) v[u] = rec[min(r + 64 * u + lane, t_hi - 1)];
+#pragma unroll
+        for (int u = 0; u < kRecUnroll; ++u)
+            if (r + 64 * u + lane < t_hi && v[u].key != 0) take_best(v[u].key, v[u].j, bk, bj);
     }
 }
 
@@ -516,10 +534,7 @@ __global__ __launch_bounds__(256) void rc_chain_kernel(const KeyTables *__restri
                 const uint64_t t_lo = (ja + kTileKeys - 1) / kTileKeys;
                 const uint64_t t_hi = (jb + 1) / kTileKeys;
                 if (t_lo < t_hi) {
-                    for (uint64_t t = t_lo + lane; t < t_hi; t += 64) {
-                        const TileRecord r = rec[tb0 + t];
-                        if (r.key != 0) take_best(r.key, r.j, bk, bj);
-                    }
+                    scan_records(rec, tb0 + t_lo, tb0 + t_hi, bk, bj);
                     scan_ranges(tl, th, base, ja, t_lo * kTileKeys - 1, t_hi * kTileKeys, jb,
                                 bk, bj);
                 } else {

@@ -23,6 +23,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+sys.path.insert(0, os.path.dirname(HERE))
 
 from replicat.utils import adapters  # noqa: E402  (reference)
 from replicat_amd import synth  # noqa: E402
@@ -241,12 +242,47 @@ def make_digests(pool, quick=False):
     return out
 
 
+# ------------------------------------------------------------- module surface
+
+from golden_surface import SURFACE_CASES, surface_call  # noqa: E402
+
+
+def make_surface():
+    # the reference's extension (oracle/_ref), loaded by path: the repository root also holds a
+    # `_replicat_adapters` (the drop-in) that must not shadow it here
+    import glob
+    import importlib.machinery
+    import importlib.util
+    so = glob.glob(os.path.join(os.path.dirname(os.path.dirname(HERE)), 'oracle', '_ref',
+                                '_replicat_adapters*.so'))[0]
+    loader = importlib.machinery.ExtensionFileLoader('_replicat_adapters', so)
+    mod = importlib.util.module_from_spec(importlib.util.spec_from_loader('_replicat_adapters', loader))
+    loader.exec_module(mod)
+    out = []
+    for name, args, call in SURFACE_CASES:
+        try:
+            r = surface_call(mod, args, call)
+            out.append({'name': name, 'args': args, 'call': call, 'result': list(r) if isinstance(r, tuple) else r,
+                        'error': None})
+        except Exception as e:  # noqa: BLE001 - recording the reference's behaviour
+            msg = str(e) if isinstance(e, ValueError) else None
+            out.append({'name': name, 'args': args, 'call': call, 'result': None,
+                        'error': type(e).__name__, 'message': msg})
+    return out
+
+
 def main():
     quick = '--quick' in sys.argv
+    if '--surface-only' in sys.argv:
+        with open(os.path.join(HERE, 'surface.json'), 'w') as f:
+            json.dump(make_surface(), f, indent=0)
+            f.write('\n')
+        return
     def dump(name, obj):
         with open(os.path.join(HERE, name), 'w') as f:
             json.dump(obj, f, separators=(',', ':'))
             f.write('\n')
+    dump('surface.json', make_surface())
     dump('small_cases.json', make_small_cases())
     dump('known_answers.json', make_known_answers())
     with mp.get_context('fork').Pool(8) as pool:
