@@ -9,7 +9,8 @@ import os
 import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, 'libreplicat_chunker.so')
+# RC_LIB_PATH: load a diagnostic build instead (profiling experiments only)
+LIB_PATH = os.environ.get('RC_LIB_PATH') or os.path.join(HERE, 'libreplicat_chunker.so')
 
 RC_OK = 0
 RC_ERR_KEY_LENGTH = 1

@@ -9,6 +9,7 @@
 #include <array>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -142,6 +143,7 @@ struct HostBuf {  // growable pinned host buffer
 
 struct rc_chunker {
     uint64_t min_length = 0, max_length = 0, window = 0;
+    uint64_t seg_force = 0, ext_steps = 2;  // segment-parallel chains (see stage_descriptors)
     uint64_t k0 = 0, k1 = 0;
     int device = 0;
     KeyTables tables;
@@ -153,6 +155,8 @@ struct rc_chunker {
         HostBuf h_desc;     // pinned staging of the descriptor arrays
         DevBuf d_desc;      // device copy
         DevBuf d_records;   // one TileRecord per tile
+        DevBuf d_scratch;   // speculative chain lists of multi-segment streams
+        DevBuf d_seg_counts;  // one count (+ termination bit) per chain segment
         hipEvent_t done = nullptr;  // the call that last used this workspace has finished
         bool pending = false;
     } ws[2];
@@ -176,11 +180,14 @@ namespace {
 
 struct Plan {
     uint64_t n = 0, n_tiles = 0, total_cap = 0;
+    uint64_t n_segs = 0, scratch_entries = 0;
+    uint64_t seg_bytes = 0, seg_cap = 0;
+    bool any_multi = false;
     size_t bytes = 0;
 };
 
 // Layout of the descriptor buffer: ptr[n] len[n] last[n] jneed[n] tile_base[n+1] cut_base[n]
-// cut_cap[n], all u64.
+// cut_cap[n] seg_base[n+1] scratch_base[n], all u64.
 StreamDesc desc_view(void *base, uint64_t n) {
     uint64_t *u = static_cast<uint64_t *>(base);
     StreamDesc d;
@@ -191,7 +198,25 @@ StreamDesc desc_view(void *base, uint64_t n) {
     d.tile_base = u + 4 * n;
     d.cut_base = u + 5 * n + 1;
     d.cut_cap = u + 6 * n + 1;
+    d.seg_base = u + 7 * n + 1;
+    d.scratch_base = u + 8 * n + 2;
     return d;
+}
+
+// Largest chunk start at which an argmax happens (S4), if any.
+bool argmax_bound(uint64_t max_length, uint64_t L, uint64_t P, uint64_t &bound) {
+    bool any = false;
+    bound = 0;
+    if (P >= max_length) {
+        any = true;
+        bound = P - max_length;
+    }
+    if (L >= 2 * max_length) {
+        const uint64_t b2 = L - 2 * max_length;
+        if (!any || b2 > bound) bound = b2;
+        any = true;
+    }
+    return any;
 }
 
 uint64_t cut_cap_of(uint64_t min_length, uint64_t L) {
@@ -226,18 +251,48 @@ Workspace &acquire_ws(rc_chunker *ch) {
 }
 
 int stage_descriptors(rc_chunker *ch, Workspace &ws, uint64_t n, const uint8_t *const *ptrs,
-                      const uint64_t *lens, const uint64_t *last, Plan &plan, bool open = false) {
+                      const uint64_t *lens, const uint64_t *last, Plan &plan, bool open = false,
+                      bool single = false) {
     plan.n = n;
-    plan.bytes = (7 * n + 1) * sizeof(uint64_t);
+    plan.bytes = (9 * n + 2) * sizeof(uint64_t);
     if (ws.pending) {  // the call that used this workspace before must be done with it
         HIP_TRY(hipEventSynchronize(ws.done));
         ws.pending = false;
     }
     if (int rc = ws.h_desc.ensure(plan.bytes)) return rc;
     uint64_t *u = static_cast<uint64_t *>(ws.h_desc.p);
-    uint64_t tiles = 0, cuts = 0;
+    // Chain segments.  The chain of a stream is one wave walking ~(bound / chunk) steps; split
+    // a stream only when the batch has too few streams to keep ~kChainWalkers waves busy, and
+    // never below 3 * max_length per segment (speculative chains must meet inside it).
+    {
+        constexpr uint64_t kChainWalkers = 1024;
+        uint64_t total = 0;
+        for (uint64_t i = 0; i < n; ++i) {
+            uint64_t b = 0;
+            const uint64_t P = open ? lens[i] : (last ? last[i] : 0);
+            if (argmax_bound(ch->max_length, lens[i], P, b)) total += b;
+        }
+        uint64_t seg = ch->seg_force ? ch->seg_force : std::max<uint64_t>(total / kChainWalkers, 1);
+        const uint64_t floor_len = ch->max_length < (1ull << 60) ? 3 * ch->max_length : ~0ull >> 2;
+        if (!ch->seg_force) seg = std::max(seg, std::max<uint64_t>(floor_len, 4ull << 20));
+        seg = std::max<uint64_t>((seg + 3) & ~3ull, 4);
+        const uint64_t step = std::max<uint64_t>(4, (ch->min_length + 3) & ~3ull);
+        plan.seg_bytes = seg;
+        plan.seg_cap = seg / step + ch->ext_steps + 4;
+    }
+    uint64_t tiles = 0, cuts = 0, segs = 0, scratch = 0;
+    plan.any_multi = false;
     for (uint64_t i = 0; i < n; ++i) {
         const uint64_t L = lens[i], P = open ? L : (last ? last[i] : 0);
+        uint64_t bound = 0, nseg = 1;
+        if (!single && argmax_bound(ch->max_length, L, P, bound)) nseg = bound / plan.seg_bytes + 1;
+        u[7 * n + 1 + i] = segs;
+        u[8 * n + 2 + i] = scratch;
+        segs += nseg;
+        if (nseg > 1) {
+            scratch += nseg * plan.seg_cap;
+            plan.any_multi = true;
+        }
         const uint64_t jneed = rc_keys_needed(ch->max_length, L, P);
         u[i] = reinterpret_cast<uint64_t>(ptrs[i]);
         u[n + i] = L;
@@ -251,8 +306,11 @@ int stage_descriptors(rc_chunker *ch, Workspace &ws, uint64_t n, const uint8_t *
         cuts += cap;
     }
     u[5 * n] = tiles;
+    u[8 * n + 1] = segs;
     plan.n_tiles = tiles;
     plan.total_cap = cuts;
+    plan.n_segs = segs;
+    plan.scratch_entries = scratch;
     return 0;
 }
 
@@ -260,6 +318,8 @@ int upload_and_launch(rc_chunker *ch, Workspace &ws, const Plan &plan, ChainPara
                       uint64_t *d_cuts, int64_t *d_counts, hipStream_t stream) {
     if (int rc = ws.d_desc.ensure(plan.bytes)) return rc;
     if (int rc = ws.d_records.ensure((plan.n_tiles + 1) * sizeof(TileRecord))) return rc;
+    if (int rc = ws.d_scratch.ensure(std::max<uint64_t>(plan.scratch_entries, 1) * 8)) return rc;
+    if (int rc = ws.d_seg_counts.ensure(std::max<uint64_t>(plan.n_segs, 1) * 8)) return rc;
     HIP_TRY(hipMemcpyAsync(ws.d_desc.p, ws.h_desc.p, plan.bytes, hipMemcpyHostToDevice, stream));
     const StreamDesc d = desc_view(ws.d_desc.p, plan.n);
     std::array<hipEvent_t, 3> ev{};
@@ -278,9 +338,10 @@ int upload_and_launch(rc_chunker *ch, Workspace &ws, const Plan &plan, ChainPara
                         static_cast<TileRecord *>(ws.d_records.p), stream))
         return fail(RC_ERR_HIP, "%s", rc_launch_error());
     if (ch->timing) HIP_TRY(hipEventRecord(ev[1], stream));
-    if (rc_launch_chain(ch->d_tables, d, plan.n, prm,
+    if (rc_launch_chain(ch->d_tables, d, plan.n, prm, plan.n_segs,
                         static_cast<const TileRecord *>(ws.d_records.p), d_cuts, d_counts,
-                        stream))
+                        static_cast<uint64_t *>(ws.d_scratch.p),
+                        static_cast<uint64_t *>(ws.d_seg_counts.p), plan.any_multi, stream))
         return fail(RC_ERR_HIP, "%s", rc_launch_error());
     HIP_TRY(hipEventRecord(ws.done, stream));
     ws.pending = true;
@@ -291,13 +352,17 @@ int upload_and_launch(rc_chunker *ch, Workspace &ws, const Plan &plan, ChainPara
     return 0;
 }
 
-ChainParams chain_params(const rc_chunker *ch, uint64_t max_steps, uint32_t flags = 0) {
+ChainParams chain_params(const rc_chunker *ch, const Plan &plan, uint64_t max_steps,
+                         uint32_t flags = 0) {
     ChainParams p;
     p.open = (flags & RC_OPEN) ? 1u : 0u;
     p.min_length = ch->min_length;
     p.max_length = ch->max_length;
     p.window = ch->window;
     p.max_steps = max_steps;
+    p.seg_bytes = plan.seg_bytes;
+    p.seg_cap = plan.seg_cap;
+    p.ext_steps = ch->ext_steps;
     return p;
 }
 
@@ -359,6 +424,13 @@ int rc_chunker_create(uint64_t min_length, uint64_t max_length, const uint8_t *k
     ch->device = device;
     build_tables(k0, k1, ch->tables);
     {
+        // chain segmentation knobs (RC_SEGMENT_BYTES forces a segment length; RC_SEGMENT_EXT
+        // sets the speculative extension); the per-call choice is made in stage_descriptors
+        if (const char *e = getenv("RC_SEGMENT_BYTES")) ch->seg_force = strtoull(e, nullptr, 0);
+        ch->ext_steps = 2;
+        if (const char *e = getenv("RC_SEGMENT_EXT")) ch->ext_steps = strtoull(e, nullptr, 0);
+    }
+    {
         DeviceGuard g(device);
         hipError_t e = hipMalloc(&ch->d_tables, sizeof(KeyTables));
         if (e == hipSuccess)
@@ -383,6 +455,8 @@ void rc_chunker_destroy(rc_chunker *ch) {
         for (auto &w : ch->ws) {
             w.d_desc.release();
             w.d_records.release();
+            w.d_scratch.release();
+            w.d_seg_counts.release();
             w.h_desc.release();
             if (w.done) (void)hipEventDestroy(w.done);
         }
@@ -474,12 +548,12 @@ int rc_next_cut(rc_chunker *ch, const uint8_t *buffer, uint64_t size, int final,
     const uint64_t L = ncopy, P = ncopy;
     Plan plan;
     Workspace &ws = acquire_ws(ch);
-    if (int rc = stage_descriptors(ch, ws, 1, &ptr, &L, &P, plan)) return rc;
+    if (int rc = stage_descriptors(ch, ws, 1, &ptr, &L, &P, plan, false, true)) return rc;
     uint64_t *d_cut = static_cast<uint64_t *>(ch->d_out.p);
     int64_t *d_count = reinterpret_cast<int64_t *>(d_cut + 1);
     const bool timing = ch->timing;
     ch->timing = false;
-    int rc = upload_and_launch(ch, ws, plan, chain_params(ch, 0), d_cut, d_count, stream);
+    int rc = upload_and_launch(ch, ws, plan, chain_params(ch, plan, 0), d_cut, d_count, stream);
     ch->timing = timing;
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(ch->h_out.p, d_cut, 16, hipMemcpyDeviceToHost, stream));
@@ -503,7 +577,7 @@ int rc_chunk_device(rc_chunker *ch, uint64_t n, const uint8_t *const *d_streams,
     Plan plan;
     Workspace &ws = acquire_ws(ch);
     if (int rc = stage_descriptors(ch, ws, n, d_streams, lens, last_piece, plan, open)) return rc;
-    return upload_and_launch(ch, ws, plan, chain_params(ch, ~0ull, flags), d_cuts, d_counts,
+    return upload_and_launch(ch, ws, plan, chain_params(ch, plan, ~0ull, flags), d_cuts, d_counts,
                              static_cast<hipStream_t>(hip_stream));
 }
 
@@ -573,7 +647,7 @@ int rc_chunk_host(rc_chunker *ch, uint64_t n, const uint8_t *const *streams, con
             return rc;
         uint64_t *dc = static_cast<uint64_t *>(ch->d_hcuts[slot].p);
         int64_t *dn = static_cast<int64_t *>(ch->d_hcounts[slot].p);
-        if (int rc = upload_and_launch(ch, ws, plan, chain_params(ch, ~0ull, flags), dc, dn, st))
+        if (int rc = upload_and_launch(ch, ws, plan, chain_params(ch, plan, ~0ull, flags), dc, dn, st))
             return rc;
         HIP_TRY(hipMemcpyAsync(cuts + cut_base[i], dc, ncut * 8, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipMemcpyAsync(counts + i, dn, nb * 8, hipMemcpyDeviceToHost, st));

@@ -46,6 +46,8 @@ struct StreamDesc {
     const uint64_t *tile_base;  // n+1 entries, exclusive prefix sum of tiles per stream
     const uint64_t *cut_base;   // n entries
     const uint64_t *cut_cap;    // n entries
+    const uint64_t *seg_base;   // n+1 entries, exclusive prefix sum of chain segments per stream
+    const uint64_t *scratch_base;  // n entries: offset of the stream's speculative lists
 };
 
 // One record per tile: first maximal key of the tile and its key index in the stream.
@@ -60,6 +62,9 @@ struct ChainParams {
     uint64_t window;      // T = (max_length - 1) / 4 keys per argmax window (0 if max < 5)
     uint64_t max_steps;   // stop after this many cuts per stream (~0 = unbounded; 0 = one raw
                           // argmax whatever its value: the single-buffer next_cut)
+    uint64_t seg_bytes;   // chain segment length (multiple of 4)
+    uint64_t seg_cap;     // entries per speculative list
+    uint64_t ext_steps;   // steps a speculative chain runs past its segment end
     uint32_t open;        // RC_OPEN: non-final prefix, no tail rule
 };
 
@@ -79,8 +84,9 @@ extern "C" {
 int rc_launch_tiles(const rc::KeyTables *d_tables, rc::StreamDesc desc, uint64_t n_streams,
                     uint64_t n_tiles, rc::TileRecord *d_records, void *stream);
 int rc_launch_chain(const rc::KeyTables *d_tables, rc::StreamDesc desc, uint64_t n_streams,
-                    rc::ChainParams prm, const rc::TileRecord *d_records, uint64_t *d_cuts,
-                    int64_t *d_counts, void *stream);
+                    rc::ChainParams prm, uint64_t n_segs, const rc::TileRecord *d_records,
+                    uint64_t *d_cuts, int64_t *d_counts, uint64_t *d_scratch,
+                    uint64_t *d_seg_counts, bool any_multi, void *stream);
 int rc_launch_fill(uint8_t *d_dst, uint64_t nbytes, uint64_t seed, uint64_t stream_id,
                    void *stream);
 const char *rc_launch_error(void);

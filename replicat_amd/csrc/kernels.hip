@@ -135,7 +135,7 @@ __device__ __forceinline__ void take_best(uint64_t k, uint64_t j, uint64_t &bk, 
 // issues all of the lane's loads -- unconditionally, at indices clamped into the range, so
 // the compiler cannot serialise them behind divergent branches -- then evaluates, so a round
 // costs one memory latency.
-constexpr int kScanUnroll = 32;
+constexpr int kScanUnroll = 16;
 
 __device__ __forceinline__ void scan_ranges(const uint64_t *tl, const uint64_t *th,
                                             const uint8_t *base, uint64_t a0, uint64_t b0,
@@ -294,14 +294,29 @@ struct TileCursor {
 };
 
 __device__ __forceinline__ void stage_tile_tables(const KeyTables *tab) {
-    // the 32x replicated prefilter tables and the exact tables
-    for (uint32_t i = threadIdx.x; i < 1024u * 32u; i += blockDim.x) {
-        const uint32_t e = i >> 5, c = i & 31, b = e >> 8, v = e & 255;
-        s_tile_lds[((b >> 1) * 65536u + v * 256u + (b & 1) * 128u) / 4 + c] = tab->pf[b][v];
+    // the 32x replicated prefilter tables and the exact tables.  Each thread loads its table
+    // entries once (all loads in flight together), then writes the 32 copies, starting at a
+    // lane-dependent copy so that a wave's stores spread over the banks.
+    const uint32_t nt = blockDim.x;
+    for (uint32_t e0 = 0; e0 < 1024u; e0 += 4 * nt) {
+        uint32_t v[4];
+        uint32_t ent[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            ent[k] = e0 + k * nt + threadIdx.x;
+            v[k] = ent[k] < 1024u ? (&tab->pf[0][0])[ent[k]] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (ent[k] >= 1024u) continue;
+            const uint32_t b = ent[k] >> 8, vv = ent[k] & 255;
+            uint32_t *row = s_tile_lds + ((b >> 1) * 65536u + vv * 256u + (b & 1) * 128u) / 4;
+            for (uint32_t c = 0; c < 32; ++c) row[(c + threadIdx.x) & 31] = v[k];
+        }
     }
     uint64_t *full = reinterpret_cast<uint64_t *>(s_tile_lds + kFullOff / 4);
     const uint64_t *gfull = &tab->tl[0][0];
-    for (uint32_t i = threadIdx.x; i < 2048u; i += blockDim.x) full[i] = gfull[i];
+    for (uint32_t i = threadIdx.x; i < 2048u; i += nt) full[i] = gfull[i];
     __syncthreads();
 }
 
@@ -482,88 +497,403 @@ __global__ __launch_bounds__(256) void rc_edge_kernel(const KeyTables *__restric
     }
 }
 
-// ----------------------------------------------------------------- phase B: chain kernel
+// ----------------------------------------------------------------- phase B: chain kernels
+//
+// The cut chain is sequential (each chunk starts at the previous cut), but the transition
+// next(s) depends on the position s only.  A stream whose argmax region spans several
+// segments of `seg_bytes` is walked segment-parallel (SURVEY.md §8 e): every segment runs a
+// SPECULATIVE chain from its own start g_i (4-aligned) through its segment and `ext_steps`
+// chunks beyond; the join kernel then follows the true chain (segment 0's) and hops onto
+// segment i's list at the first position both chains share -- from there the two are the
+// same chain.  Chains normally meet within a chunk; if a list runs out first, the join kernel
+// computes the missing steps itself, so the result is exact in every case.
 
-__global__ __launch_bounds__(256) void rc_chain_kernel(const KeyTables *__restrict__ tab,
-                                                       StreamDesc d, uint64_t n_streams,
-                                                       ChainParams prm,
-                                                       const TileRecord *__restrict__ rec,
-                                                       uint64_t *__restrict__ cuts,
-                                                       int64_t *__restrict__ counts) {
-    __shared__ __attribute__((aligned(16))) uint64_t s_full[2048];
-    const uint64_t *gfull = &tab->tl[0][0];
-    for (uint32_t i = threadIdx.x; i < 2048u; i += blockDim.x) s_full[i] = gfull[i];
-    __syncthreads();
-    const uint64_t *tl = s_full, *th = s_full + 1024;
+struct ChainStream {
+    const uint8_t *base;
+    uint64_t L, P, tb0, jmax;
+#ifdef RC_DIAG_STAMPS
+    bool diag;
+#endif
+};
 
+__device__ __forceinline__ ChainStream chain_stream(const StreamDesc &d, uint64_t s) {
+    ChainStream st;
+    st.base = sload_ptr(d.ptr + s);
+    st.L = sload(d.len + s);
+    st.P = sload(d.last + s);
+    st.tb0 = sload(d.tile_base + s);
+    st.jmax = st.L >= 8 ? (st.L - 4) / 4 : 0;
+#ifdef RC_DIAG_STAMPS
+    st.diag = s == 0;
+#endif
+    return st;
+}
+
+// Top-16 scan of the window's two partial edge tiles, keys [a0, b0] then [a1, b1] (either
+// may be empty), with the conflict-free prefilter tables -- the tile kernel's inner loop on an
+// unaligned key range: each lane takes 4 consecutive words per 256-key iteration, the word
+// before a lane's first key comes from the previous lane by DPP.  Per lane: running maxima of
+// (top16 << 16 | valid 0x8000 | order) for the first and the last occurrence; the order is the
+// lane-local key index (0-255 head, 256-511 tail; a range holds at most 8190 keys).
+constexpr int kEdgeIters = 8;  // 256-key iterations whose loads are issued together
+
+__device__ __forceinline__ void edge_prefilter(const uint8_t *base, uint64_t wmax, uint64_t a0,
+                                               uint64_t b0, uint64_t a1, uint64_t b1,
+                                               uint32_t lb_a, uint32_t lb_b, uint32_t &acc_first,
+                                               uint32_t &acc_last) {
     const uint32_t lane = lane_id();
-    const uint64_t s = (uint64_t)blockIdx.x * (blockDim.x >> 6) +
-                       __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (s >= n_streams) return;
+    acc_first = acc_last = 0;
+#pragma unroll 1
+    for (int R = 0; R < 2; ++R) {
+        const uint64_t a = R ? a1 : a0, b = R ? b1 : b0;
+        if (a > b) continue;
+        const uint64_t q0 = a & ~3ull;                   // first word of iteration 0
+        const uint32_t nk = (uint32_t)(b - q0);          // last key offset from q0
+        const uint8_t *p = base + 4 * q0;
+        const uint32_t wlast = (uint32_t)(wmax - q0);    // last existing word, from q0
+        uint32_t carry = pf_entry(ld_u32(base + 4 * (q0 ? q0 - 1 : 0)), lb_a, lb_b);
+        for (uint32_t it0 = 0; it0 * 256 <= nk; it0 += kEdgeIters) {
+            uint32_t w[kEdgeIters][4];
+#pragma unroll
+            for (int i = 0; i < kEdgeIters; ++i)
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    w[i][k] = ld_u32(p + 4 * min((it0 + i) * 256 + lane * 4 + k, wlast));
+#pragma unroll
+            for (int i = 0; i < kEdgeIters; ++i) {
+                const uint32_t it = it0 + i;
+                uint32_t ad[16];
+                pf_addrs(w[i][0], lb_a, lb_b, ad + 0);
+                pf_addrs(w[i][1], lb_a, lb_b, ad + 4);
+                pf_addrs(w[i][2], lb_a, lb_b, ad + 8);
+                pf_addrs(w[i][3], lb_a, lb_b, ad + 12);
+                const uint32_t e0 = pf_gather(ad + 0), e1 = pf_gather(ad + 4);
+                const uint32_t e2 = pf_gather(ad + 8), e3 = pf_gather(ad + 12);
+                const uint32_t rot = __builtin_amdgcn_update_dpp(0u, e3, 0x13C, 0xf, 0xf, false);
+                const uint32_t ep = lane == 0 ? carry : rot;
+                carry = rot;
+                const uint32_t t[4] = {(ep & 0xffff0000u) ^ (e0 << 16), (e0 & 0xffff0000u) ^ (e1 << 16),
+                                       (e1 & 0xffff0000u) ^ (e2 << 16), (e2 & 0xffff0000u) ^ (e3 << 16)};
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t off = it * 256 + lane * 4 + k;   // key q0 + off
+                    const bool valid = off <= nk && q0 + off >= a;
+                    const uint32_t local = 256u * R + it * 4 + k;
+                    acc_first = max3_u32(acc_first, valid ? (t[k] | 0x8000u | (511u - local)) : 0u, 0u);
+                    acc_last = max3_u32(acc_last, valid ? (t[k] | 0x8000u | local) : 0u, 0u);
+                }
+            }
+        }
+    }
+}
 
-    const uint8_t *base = d.ptr[s];
-    const uint64_t L = d.len[s], P = d.last[s], tb0 = d.tile_base[s];
-    const uint64_t cbase = d.cut_base[s], cap = d.cut_cap[s];
+enum : int { kStepStop = 0, kStepCut = 1, kStepTail1 = 2, kStepTail2 = 3 };
+
+#ifdef RC_DIAG_STAMPS
+// diagnostic build only: per-step s_memrealtime stamps (100 MHz) of stream 0's walker
+__device__ uint64_t g_diag[4096];
+__device__ uint32_t g_diag_n;
+#define RC_STAMP(tag)                                                                  \
+    do {                                                                               \
+        if (st.diag && lane_id() == 0 && g_diag_n < 4000) {                            \
+            g_diag[g_diag_n++] = ((uint64_t)(tag) << 56) | __builtin_amdgcn_s_memrealtime(); \
+        }                                                                              \
+    } while (0)
+#else
+#define RC_STAMP(tag) \
+    do {              \
+    } while (0)
+#endif
+
+// One chain step from chunk start `pos` (< L): an argmax cut (adapters.cpp:59-69), or the tail
+// rule's one or two final cuts (adapters.cpp:48-55), or stop (non-final wait / S7 UB).
+// prm.max_steps == 0 is the raw single next_cut: c1 = the argmax offset, whatever its value.
+__device__ int chain_step(const uint64_t *tl, const uint64_t *th, const TileRecord *rec,
+                          const ChainStream &st, const ChainParams &prm, uint64_t pos,
+                          uint32_t lb_a, uint32_t lb_b, uint64_t &c1, uint64_t &c2) {
     const uint64_t minl = prm.min_length, maxl = prm.max_length, T = prm.window;
-    const uint64_t jmax = L >= 8 ? (L - 4) / 4 : 0;
-    const uint64_t forced = (minl + 3) & ~3ull;
-    const bool single = prm.max_steps == 0;  // raw next_cut: one argmax, result even if 0
+    const bool single = prm.max_steps == 0;
+    const uint64_t rem = st.L - pos;
+    const bool argmax = single || (st.P >= pos && st.P - pos >= maxl) || rem >= 2 * maxl;
+    if (prm.open && !argmax) return kStepStop;  // a non-final next_cut returns 0: wait
+    if (argmax) {
+        // window keys j in [pos/4 + 1, pos/4 + T]  (i = 4 .. < max, adapters.cpp:59): the full
+        // tiles inside it come from their records (exact keys); the two partial edge tiles are
+        // scanned at top-16 precision and only their candidates get exact keys -- and only if
+        // they can beat the records (the records hold ~99 % of a default-size window).
+        const uint64_t s4 = pos >> 2;
+        const uint64_t ja = s4 + 1, jb = min(s4 + T, st.jmax);
+        uint64_t bk = 0, bj = ~0ull;
+        RC_STAMP(1);
+        if (T > 0 && ja <= jb) {
+            const uint64_t t_lo = (ja + kTileKeys - 1) / kTileKeys;
+            const uint64_t t_hi = (jb + 1) / kTileKeys;
+            uint64_t a0 = ja, b0 = jb, a1 = 1, b1 = 0;
+            if (t_lo < t_hi) {
+#ifndef RC_DIAG_SKIP_RECORDS
+                scan_records(rec, st.tb0 + t_lo, st.tb0 + t_hi, bk, bj);
+#endif
+                b0 = t_lo * kTileKeys - 1;
+                a1 = t_hi * kTileKeys;
+                b1 = jb;
+            }
+            wave_best(bk, bj);
+            RC_STAMP(2);
+            uint32_t acc_first = 0, acc_last = 0;
+#ifndef RC_DIAG_SKIP_EDGES
+            edge_prefilter(st.base, st.L / 4 - 1, a0, b0, a1, b1, lb_a, lb_b, acc_first, acc_last);
+#endif
+            RC_STAMP(3);
+            const uint32_t m = wave_max_u32(acc_first);
+            if ((m & 0x8000u) && (m >> 16) >= (uint32_t)(bk >> 48)) {
+                const bool cand = (acc_first >> 16) == (m >> 16) && (acc_first & 0x8000u);
+                const uint32_t fl = 511u - (acc_first & 0x1ffu), ll = acc_last & 0x1ffu;
+                if (__any(cand && fl != ll)) {
+                    // a candidate lane holds its top-16 maximum twice: exact scan of the edges
+                    uint64_t ek = 0, ej = ~0ull;
+                    scan_ranges(tl, th, st.base, a0, b0, a1, b1, ek, ej);
+                    take_best(ek, ej, bk, bj);
+                    wave_best(bk, bj);
+                } else {
+                    const uint32_t lo = fl & 255u;  // lane-local index within its range
+                    const uint64_t jc = ((fl < 256 ? a0 : a1) & ~3ull) + 256ull * (lo >> 2) +
+                                        4ull * lane_id() + (lo & 3);
+                    const uint64_t jl = cand ? jc : (uint64_t)a0;  // any valid index
+                    const uint64_t k = full_key(tl, th, ld_u32(st.base + 4 * jl - 4),
+                                                ld_u32(st.base + 4 * jl));
+                    for (uint64_t cm = __ballot(cand); cm; cm &= cm - 1) {
+                        const int l = __builtin_ctzll(cm);
+                        take_best(lane_u64(k, l), lane_u64(jl, l), bk, bj);
+                    }
+                }
+            }
+        }
+        RC_STAMP(4);
+        uint64_t idx = bk > 0 ? 4 * (bj - s4) : 0;
+        if (idx < minl) idx = (minl + 3) & ~3ull;  // adapters.cpp:66-67
+        if (single) {
+            c1 = idx;
+            return kStepCut;
+        }
+        if (idx != 0) {
+            c1 = pos + idx;
+            return kStepCut;
+        }
+        if (rem >= 2 * maxl || prm.open) return kStepStop;  // min_length == 0 (S7 UB)
+    }
+    uint64_t c;
+    if (rem <= maxl) c = rem;
+    else if (rem < maxl + minl) c = rem / 2;
+    else c = maxl;
+    if (c == 0) return kStepStop;
+    c1 = pos + c;
+    if (c < rem) {
+        c2 = st.L;
+        return kStepTail2;
+    }
+    return kStepTail1;
+}
 
-    uint64_t pos = 0, n = 0;
-    bool overflow = false;
+__device__ __forceinline__ uint64_t find_index(const uint64_t *base_arr, uint64_t n, uint64_t v) {
+    uint64_t lo = 0, hi = n;  // largest i with base_arr[i] <= v
+    while (hi - lo > 1) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (sload(base_arr + mid) <= v) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// Spec kernel: one wave per segment.  A one-segment stream writes its final cuts directly;
+// segment i of a longer stream writes its list to the scratch and its count (bit 63 set if the
+// chain ended inside the list: tail rule or stop).
+__global__ __launch_bounds__(256) void rc_spec_kernel(const KeyTables *__restrict__ tab,
+                                                      StreamDesc d, uint64_t n_streams,
+                                                      ChainParams prm, uint64_t n_segs,
+                                                      const TileRecord *__restrict__ rec,
+                                                      uint64_t *__restrict__ cuts,
+                                                      int64_t *__restrict__ counts,
+                                                      uint64_t *__restrict__ scratch,
+                                                      uint64_t *__restrict__ seg_counts) {
+    stage_tile_tables(tab);
+    const uint64_t *full = reinterpret_cast<const uint64_t *>(s_tile_lds + kFullOff / 4);
+    const uint64_t *tl = full, *th = full + 1024;
+    const uint32_t lane = lane_id();
+    const uint32_t lb_a = (lane & 31) * 4, lb_b = lb_a | 0x10000u;
+    const uint64_t q = (uint64_t)blockIdx.x * (blockDim.x >> 6) +
+                       __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (q >= n_segs) return;
+    const uint64_t s = find_index(d.seg_base, n_streams + 1, q);
+    const uint64_t sb = sload(d.seg_base + s), nseg = sload(d.seg_base + s + 1) - sb;
+    const uint64_t i = q - sb;
+    const ChainStream st = chain_stream(d, s);
+    const bool direct = nseg == 1;
+    uint64_t *out = direct ? cuts + sload(d.cut_base + s) : scratch + sload(d.scratch_base + s) + i * prm.seg_cap;
+    const uint64_t cap = direct ? sload(d.cut_cap + s) : prm.seg_cap;
+    const uint64_t seg_end = (i + 1) * prm.seg_bytes;
+    const uint64_t steps = prm.max_steps == 0 ? 1 : prm.max_steps;
+
+    uint64_t pos = i * prm.seg_bytes, n = 0, ext = 0;
+    bool overflow = false, term = false;
     auto emit = [&](uint64_t c) {
         if (n >= cap) {
             overflow = true;
             return;
         }
-        if (lane == 0) cuts[cbase + n] = c;
+        if (lane == 0) out[n] = c;
         ++n;
     };
-    const uint64_t steps = single ? 1 : prm.max_steps;
+    for (;;) {
+        if (pos >= st.L || n >= steps) {
+            term = true;
+            break;
+        }
+        if (!direct && pos >= seg_end && ext++ >= prm.ext_steps) break;
+        uint64_t c1 = 0, c2 = 0;
+        const int kind = chain_step(tl, th, rec, st, prm, pos, lb_a, lb_b, c1, c2);
+        if (kind == kStepStop) {
+            term = true;
+            break;
+        }
+        emit(c1);
+        if (kind == kStepTail2) emit(c2);
+        if (kind != kStepCut) {
+            term = true;
+            break;
+        }
+        if (overflow) break;
+        pos = c1;
+    }
+    if (lane == 0) {
+        if (direct) counts[s] = overflow ? -1 : (int64_t)n;
+        else seg_counts[q] = overflow ? ~0ull : (n | (term ? (1ull << 63) : 0));
+    }
+}
 
-    while (pos < L && n < steps && !overflow) {
-        const uint64_t rem = L - pos;
-        const bool argmax = single || (P >= pos && P - pos >= maxl) || rem >= 2 * maxl;
-        if (prm.open && !argmax) break;  // a non-final next_cut returns 0: wait for more bytes
-        if (argmax) {
-            // window keys j in [pos/4 + 1, pos/4 + T]  (i = 4 .. < max, adapters.cpp:59)
-            const uint64_t s4 = pos >> 2;
-            const uint64_t ja = s4 + 1, jb = min(s4 + T, jmax);
-            uint64_t bk = 0, bj = ~0ull;
-            if (T > 0 && ja <= jb) {
-                const uint64_t t_lo = (ja + kTileKeys - 1) / kTileKeys;
-                const uint64_t t_hi = (jb + 1) / kTileKeys;
-                if (t_lo < t_hi) {
-                    scan_records(rec, tb0 + t_lo, tb0 + t_hi, bk, bj);
-                    scan_ranges(tl, th, base, ja, t_lo * kTileKeys - 1, t_hi * kTileKeys, jb,
-                                bk, bj);
-                } else {
-                    scan_ranges(tl, th, base, ja, jb, 1, 0, bk, bj);
-                }
-                wave_best(bk, bj);
-            }
-            uint64_t idx = bk > 0 ? 4 * (bj - s4) : 0;
-            if (idx < minl) idx = forced;  // adapters.cpp:66-67
-            if (single) {
-                emit(idx);
+// Join kernel: one wave per multi-segment stream, following the true chain across the
+// speculative lists (see above).
+__global__ __launch_bounds__(256) void rc_join_kernel(const KeyTables *__restrict__ tab,
+                                                      StreamDesc d, uint64_t n_streams,
+                                                      ChainParams prm,
+                                                      const TileRecord *__restrict__ rec,
+                                                      uint64_t *__restrict__ cuts,
+                                                      int64_t *__restrict__ counts,
+                                                      const uint64_t *__restrict__ scratch,
+                                                      const uint64_t *__restrict__ seg_counts) {
+    stage_tile_tables(tab);
+    const uint64_t *full = reinterpret_cast<const uint64_t *>(s_tile_lds + kFullOff / 4);
+    const uint64_t *tl = full, *th = full + 1024;
+    const uint32_t lane = lane_id();
+    const uint32_t lb_a = (lane & 31) * 4, lb_b = lb_a | 0x10000u;
+    const uint64_t s = (uint64_t)blockIdx.x * (blockDim.x >> 6) +
+                       __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (s >= n_streams) return;
+    const uint64_t sb = sload(d.seg_base + s), nseg = sload(d.seg_base + s + 1) - sb;
+    if (nseg <= 1) return;  // written directly by the spec kernel
+    const ChainStream st = chain_stream(d, s);
+    uint64_t *out = cuts + sload(d.cut_base + s);
+    const uint64_t cap = sload(d.cut_cap + s);
+    const uint64_t *lists = scratch + sload(d.scratch_base + s);
+    const uint64_t S = prm.seg_bytes;
+
+    auto list_of = [&](uint64_t k) { return lists + k * prm.seg_cap; };
+    auto count_of = [&](uint64_t k, bool &term, bool &bad) {
+        const uint64_t c = seg_counts[sb + k];
+        bad = c == ~0ull;
+        term = (c >> 63) != 0;
+        return c & ~(1ull << 63);
+    };
+
+    uint64_t pos = 0, n = 0, src = 0, idx = 0;
+    bool overflow = false, src_term, bad;
+    uint64_t src_cnt = count_of(0, src_term, bad);
+    overflow |= bad;
+    while (!overflow) {
+        // bulk: the source list's entries below the next segment's start need no checks
+        const uint64_t g_next = src + 1 < nseg ? (src + 1) * S : ~0ull;
+        const uint64_t *lst = list_of(src);
+        for (;;) {
+            const uint64_t k = idx + lane;
+            const uint64_t v = k < src_cnt ? lst[k] : ~0ull;
+            const uint64_t take = __ballot(v < g_next);
+            const uint32_t m = __popcll(take);  // sorted list: a prefix
+            if (m == 0) break;
+            if (n + m > cap) {
+                overflow = true;
                 break;
             }
-            if (idx != 0) {
-                pos += idx;
-                emit(pos);
-                continue;
-            }
-            if (rem >= 2 * maxl || prm.open) break;  // min_length == 0, no positive key (S7 UB)
+            if (v < g_next) out[n + lane] = v;
+            n += m;
+            idx += m;
+            pos = lane_u64(v, m - 1);
+            if (m < 64) break;
         }
-        // tail rule of a final buffer < 2*max (adapters.cpp:48-55): one or two chunks
-        uint64_t c;
-        if (rem <= maxl) c = rem;
-        else if (rem < maxl + minl) c = rem / 2;
-        else c = maxl;
-        if (c == 0) break;
-        emit(pos + c);
-        if (c < rem) emit(L);
-        break;
+        if (overflow) break;
+        if (idx >= src_cnt && src_term) break;  // the true chain ended inside this list
+        // hop: is `pos` a position of a later segment's speculative chain?
+        bool hopped = false;
+        const uint64_t kmax = min(pos / S, nseg - 1);
+        for (uint64_t k = src + 1; k <= kmax && !hopped; ++k) {
+            bool kt, kb;
+            const uint64_t kc = count_of(k, kt, kb);
+            if (kb) {
+                overflow = true;
+                break;
+            }
+            if (pos == k * S) {  // the speculative start itself
+                hopped = true;
+                src = k;
+                idx = 0;
+                src_cnt = kc;
+                src_term = kt;
+                break;
+            }
+            const uint64_t *kl = list_of(k);
+            for (uint64_t w = 0; w < kc; w += 64) {
+                const uint64_t v = w + lane < kc ? kl[w + lane] : ~0ull;
+                const uint64_t hit = __ballot(v == pos);
+                if (hit) {
+                    hopped = true;
+                    src = k;
+                    idx = w + __builtin_ctzll(hit) + 1;
+                    src_cnt = kc;
+                    src_term = kt;
+                    break;
+                }
+                if (lane_u64(v, 63) > pos || w + 64 >= kc) break;  // sorted: no later match
+            }
+        }
+        if (overflow) break;
+        if (hopped) continue;
+        // no hop: follow the current list one entry, or compute the step when it ran out
+        if (idx < src_cnt) {
+            const uint64_t v = lst[idx++];
+            if (n >= cap) {
+                overflow = true;
+                break;
+            }
+            if (lane == 0) out[n] = v;
+            ++n;
+            pos = v;
+            if (idx >= src_cnt && src_term) break;
+            continue;
+        }
+        if (pos >= st.L) break;
+        uint64_t c1 = 0, c2 = 0;
+        const int kind = chain_step(tl, th, rec, st, prm, pos, lb_a, lb_b, c1, c2);
+        if (kind == kStepStop) break;
+        if (n + (kind == kStepTail2 ? 2 : 1) > cap) {
+            overflow = true;
+            break;
+        }
+        if (lane == 0) {
+            out[n] = c1;
+            if (kind == kStepTail2) out[n + 1] = c2;
+        }
+        n += kind == kStepTail2 ? 2 : 1;
+        if (kind != kStepCut) break;
+        pos = c1;
+        src_cnt = idx;  // nothing left to follow in the current list
     }
     if (lane == 0) counts[s] = overflow ? -1 : (int64_t)n;
 }
@@ -604,6 +934,18 @@ extern "C" {
 
 const char *rc_launch_error(void) { return g_launch_err; }
 
+#ifdef RC_DIAG_STAMPS
+int rc_diag_read(uint64_t *out, uint32_t cap, uint32_t *n) {
+    uint32_t k = 0;
+    if (hipMemcpyFromSymbol(&k, HIP_SYMBOL(g_diag_n), 4) != hipSuccess) return 1;
+    if (k > cap) k = cap;
+    if (k && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag), k * 8) != hipSuccess) return 1;
+    *n = k;
+    const uint32_t z = 0;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_diag_n), &z, 4) != hipSuccess;
+}
+#endif
+
 int rc_launch_tiles(const KeyTables *d_tables, StreamDesc desc, uint64_t n_streams,
                     uint64_t n_tiles, TileRecord *d_records, void *stream) {
     if (n_tiles == 0) return 0;
@@ -625,14 +967,22 @@ int rc_launch_tiles(const KeyTables *d_tables, StreamDesc desc, uint64_t n_strea
 }
 
 int rc_launch_chain(const KeyTables *d_tables, StreamDesc desc, uint64_t n_streams,
-                    ChainParams prm, const TileRecord *d_records, uint64_t *d_cuts,
-                    int64_t *d_counts, void *stream) {
+                    ChainParams prm, uint64_t n_segs, const TileRecord *d_records,
+                    uint64_t *d_cuts, int64_t *d_counts, uint64_t *d_scratch,
+                    uint64_t *d_seg_counts, bool any_multi, void *stream) {
     if (n_streams == 0) return 0;
-    const uint64_t grid = (n_streams + kChainWaves - 1) / kChainWaves;
-    hipLaunchKernelGGL(rc_chain_kernel, dim3((unsigned)grid), dim3(kChainWaves * kWaveSize), 0,
-                       (hipStream_t)stream, d_tables, desc, n_streams, prm, d_records, d_cuts,
-                       d_counts);
-    return launch_status("rc_chain_kernel");
+    hipStream_t st = (hipStream_t)stream;
+    const uint64_t grid = (n_segs + kChainWaves - 1) / kChainWaves;
+    hipLaunchKernelGGL(rc_spec_kernel, dim3((unsigned)grid), dim3(kChainWaves * kWaveSize), 0, st,
+                       d_tables, desc, n_streams, prm, n_segs, d_records, d_cuts, d_counts,
+                       d_scratch, d_seg_counts);
+    if (launch_status("rc_spec_kernel")) return 1;
+    if (!any_multi) return 0;
+    const uint64_t jgrid = (n_streams + kChainWaves - 1) / kChainWaves;
+    hipLaunchKernelGGL(rc_join_kernel, dim3((unsigned)jgrid), dim3(kChainWaves * kWaveSize), 0, st,
+                       d_tables, desc, n_streams, prm, d_records, d_cuts, d_counts,
+                       (const uint64_t *)d_scratch, (const uint64_t *)d_seg_counts);
+    return launch_status("rc_join_kernel");
 }
 
 int rc_launch_fill(uint8_t *d_dst, uint64_t nbytes, uint64_t seed, uint64_t stream_id,

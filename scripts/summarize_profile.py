@@ -16,7 +16,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def short(name):
-    for k in ('rc_tile_kernel', 'rc_edge_kernel', 'rc_chain_kernel', 'rc_fill_kernel'):
+    for k in ('rc_tile_kernel', 'rc_edge_kernel', 'rc_chain_kernel', 'rc_spec_kernel',
+              'rc_join_kernel', 'rc_fill_kernel'):
         if k in name:
             return k
     return name[:60]

@@ -268,3 +268,50 @@ def test_tile_records_vs_oracle(kind):
         assert bad.size == 0, (kind, n, bad[:8].tolist(), gk[bad[:4]].tolist(), ek[bad[:4]].tolist(),
                                gj[bad[:4]].tolist(), ej[bad[:4]].tolist())
         base += nt
+
+
+@pytest.mark.parametrize('seg_bytes,ext', [(1 << 16, 0), (1 << 16, 1), (1 << 16, 4),
+                                           (12 * 4096, 2), (1 << 20, 3)])
+def test_segmented_chains_vs_oracle(monkeypatch, seg_bytes, ext):
+    """Segment-parallel speculative chains + join, with tiny segments and short extensions
+    (ext 0 forces the join kernel to compute most steps itself)."""
+    o = _oracle()
+    monkeypatch.setenv('RC_SEGMENT_BYTES', str(seg_bytes))
+    monkeypatch.setenv('RC_SEGMENT_EXT', str(ext))
+    rnd = random.Random(seg_bytes + ext)
+    for trial in range(3):
+        mx = rnd.choice([4096, 16384, 4096 * 3])
+        mn = rnd.choice([4, 500, mx // 2, mx])
+        key = rnd.randbytes(16) if trial else b'\xff' * 16
+        if key[:8] == bytes(8):
+            key = b'\x01' + key[1:]
+        ch = GpuChunker(mn, mx, key)
+        sizes, datas, last = [], [], []
+        for k in range(12):
+            n = rnd.choice([rnd.randrange(0, 3 << 20), 2 << 20, (1 << 20) + 3, 7 * mx])
+            kind = k % 4
+            if kind == 0:
+                d = np.frombuffer(rnd.randbytes(n), np.uint8)
+            elif kind == 1:
+                d = np.zeros(n, np.uint8)
+            elif kind == 2:
+                d = np.resize(np.frombuffer(rnd.randbytes(rnd.randrange(1, 9000)), np.uint8), n)
+            else:
+                d = synth.stream_bytes(n, synth.DEFAULT_SEED, 500 + k)
+            sizes.append(n)
+            datas.append(d)
+            last.append(rnd.choice([0, n, rnd.randrange(0, n + 1)]))
+        ts = device_streams(sizes, datas=datas)
+        got = chunk_device(ch, ts, sizes, last)
+        for d, P, g in zip(datas, last, got):
+            assert g == o.chunk_stream(d, mn, mx, key, P), (mn, mx, len(d), P)
+        got_open = chunk_device(ch, ts, sizes, None, open_=True)
+        for d, g in zip(datas, got_open):
+            full = o.chunk_stream(d, mn, mx, key, len(d))
+            exp, s = [], 0
+            for e in full:
+                if len(d) - s < mx:
+                    break
+                exp.append(e)
+                s = e
+            assert g == exp
