@@ -34,8 +34,14 @@ def parse():
     p.add_argument('--gpus', type=int, default=1)
     p.add_argument('--steps', type=int, default=10)
     p.add_argument('--warmup', type=int, default=2)
-    p.add_argument('--streams', type=int, default=1024)
-    p.add_argument('--stream-mib', type=int, default=64)
+    p.add_argument('--config', choices=['2', '3i', '3iii', '4'], default='2',
+                   help='2: 1024 x 64 MiB (the metric); 3i: 65536 x 1 MiB default params '
+                        '(degenerate: tail rule only); 3iii: 65536 x 1 MiB, min 2000 / max 80000; '
+                        '4: 16 x 8 GiB per GPU (streams rank, rank+8, ...)')
+    p.add_argument('--streams', type=int, default=None)
+    p.add_argument('--stream-mib', type=int, default=None)
+    p.add_argument('--calibrate', action='store_true',
+                   help='also time a pure streaming read of the same bytes (rc_read_probe)')
     p.add_argument('--key', choices=['ff', 'seeded'], default='ff')
     p.add_argument('--cpu-streams', type=int, default=256,
                    help='bounded CPU-baseline sample (64 MiB streams); 0 = skip')
@@ -132,17 +138,20 @@ def main():
         dist.init_process_group('nccl', device_id=torch.device('cuda', local))
 
     from replicat_amd import synth
-    from replicat_amd.chunker import GpuChunker, fill_splitmix
+    from replicat_amd.chunker import GpuChunker, fill_splitmix, read_probe
     key = b'\xff' * 16 if args.key == 'ff' else synth.seeded_key(1)
-    ch = GpuChunker(MIN_LEN, MAX_LEN, key, device=local)
-
-    n, size = args.streams, args.stream_mib << 20
+    cfg = {'2': (1024, 64, MIN_LEN, MAX_LEN), '3i': (65536, 1, MIN_LEN, MAX_LEN),
+           '3iii': (65536, 1, 2_000, 80_000), '4': (16, 8192, MIN_LEN, MAX_LEN)}[args.config]
+    n = args.streams or cfg[0]
+    size = (args.stream_mib or cfg[1]) << 20
+    min_len, max_len = cfg[2], cfg[3]
+    ch = GpuChunker(min_len, max_len, key, device=local)
     stream = torch.cuda.current_stream()
     hs = stream.cuda_stream
     pool = torch.empty(n * size, dtype=torch.uint8, device='cuda')  # one 16-B aligned arena
     base_ptr = pool.data_ptr()
     ptrs = [base_ptr + i * size for i in range(n)]
-    ids = [rank * n + i for i in range(n)]
+    ids = [rank + 8 * i for i in range(n)] if args.config == '4' else [rank * n + i for i in range(n)]
     for p, i in zip(ptrs, ids):
         fill_splitmix(p, size, synth.DEFAULT_SEED, i, hs)
     lens = [size] * n
@@ -190,15 +199,17 @@ def main():
         sys.path.insert(0, os.path.join(ROOT, 'tests'))
         import golden_util as G
         gold = {d['name']: d for d in G.load('digests.json')}
-        if args.key == 'ff' and n == 1024 and size == 64 << 20:
+        if args.key == 'ff' and n == 1024 and size == 64 << 20 and args.config == '2':
             parity = digest == gold['config2_ff']['sha256']
+        elif args.key == 'ff' and args.config == '3iii' and n >= 4096:
+            parity = G.cutlist_digest(ends[:4096]) == gold['config3iii_first4096']['sha256']
     if world > 1:
         dist.barrier()
 
     result = None
     if rank == 0:
         cpu = None
-        if args.cpu_streams and world == 1 and args.key == 'ff':
+        if args.cpu_streams and world == 1 and args.key == 'ff' and args.config == '2':
             cpu, cpu_ends = cpu_baseline(min(args.cpu_streams, n), size, synth.DEFAULT_SEED,
                                          args.cpu_procs)
             if ends is not None:
@@ -206,14 +217,35 @@ def main():
                            for i in cpu_ends)
                 cpu['matches_gpu'] = bool(same)
         e2e = None
-        if args.e2e:
-            hbufs = [synth.stream_bytes(size, synth.DEFAULT_SEED, i) for i in range(16)]
-            ch.chunk_host(hbufs[:2])
-            t1 = time.perf_counter()
-            ch.chunk_host(hbufs)
-            e2e = round(16 * size / (time.perf_counter() - t1) / GIB, 2)
+        if args.e2e:  # host-resident streams: copies in, chunking, cut offsets out
+            m = min(n, 64)
+            hbufs = [synth.stream_bytes(size, synth.DEFAULT_SEED, i) for i in range(m)]
+            pinned = torch.empty(m * size, dtype=torch.uint8).pin_memory()
+            pv = pinned.numpy()
+            for i, b in enumerate(hbufs):
+                pv[i * size:(i + 1) * size] = b
+            pbufs = [pv[i * size:(i + 1) * size] for i in range(m)]
+            e2e = {}
+            for label, bufs in (('pageable', hbufs), ('pinned', pbufs)):
+                ch.chunk_host(bufs[:2])
+                t1 = time.perf_counter()
+                ch.chunk_host(bufs)
+                e2e[label] = round(m * size / (time.perf_counter() - t1) / GIB, 2)
+            e2e['streams'] = m
+        calib = None
+        if args.calibrate:
+            out = torch.zeros(4, dtype=torch.int32, device='cuda')
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            for _ in range(2):
+                read_probe(base_ptr, n * size, out.data_ptr(), hs)
+            ev0.record(stream)
+            for _ in range(5):
+                read_probe(base_ptr, n * size, out.data_ptr(), hs)
+            ev1.record(stream)
+            torch.cuda.synchronize()
+            calib = round(5 * n * size / (ev0.elapsed_time(ev1) * 1e-3) / 1e9, 1)
         result = {
-            'metric': 'GiB/s chunked, device-resident streams (config 2: 1024 x 64 MiB per GPU)',
+            'metric': 'GiB/s chunked, device-resident streams',
             'value': round(value, 2),
             'unit': 'GiB/s',
             'n_gpus': world,
@@ -225,16 +257,18 @@ def main():
             'vs_baseline': None,
             'dtype': 'u8',
             'data': 'synthetic (splitmix64 counter streams generated in HBM)',
-            'config': {'workload': 'config2: %d x %d MiB streams per GPU, min %d, max %d, key %s'
-                                   % (n, size >> 20, MIN_LEN, MAX_LEN, args.key),
+            'config': {'workload': 'config%s: %d x %d MiB streams per GPU, min %d, max %d, key %s'
+                                   % (args.config, n, size >> 20, min_len, max_len, args.key),
                        'streams_per_gpu': n, 'stream_bytes': size, 'parallelism': f'streams/{world} ranks'},
             'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
                          'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4),
                          'traffic': None, 'kernel': 'rc_tile_kernel',
                          'kernel_ms': round(a_avg, 3), 'chain_kernel_ms': round(b_avg, 3)},
             'cpu_baseline': cpu,
-            'parity_config2_sha256': parity,
+            'parity_sha256': parity,
         }
+        if calib is not None:
+            result['read_probe_gbs'] = calib
         if e2e is not None:
             result['e2e_host_gibs'] = e2e
         print(json.dumps(result), flush=True)

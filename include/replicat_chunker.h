@@ -108,6 +108,12 @@ int rc_timing_read(rc_chunker *ch, double *phase_a_ms, double *phase_b_ms, uint6
 int rc_fill_splitmix(uint8_t *d_dst, uint64_t nbytes, uint64_t seed, uint64_t stream,
                      void *hip_stream);
 
+/* Calibration (bench.py --calibrate): stream the first nbytes (whole 16 KiB tiles) of a
+ * 16-byte aligned device buffer with the tile kernel's exact load pattern and no hashing; its
+ * rate is the attainable streaming-read ceiling for the tile kernel on this device.
+ * Enqueue only. */
+int rc_read_probe(const uint8_t *d_src, uint64_t nbytes, uint32_t *d_out, void *hip_stream);
+
 /* Keys j (key j covers bytes [4j-4, 4j+4)) that any argmax window of a stream (L, P) can
  * reach: the largest such j, or 0 when the stream never hashes (tail rule only). */
 uint64_t rc_keys_needed(uint64_t max_length, uint64_t L, uint64_t P);

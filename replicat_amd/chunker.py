@@ -144,6 +144,10 @@ def fill_splitmix(ptr, nbytes, seed, stream_id, hip_stream=0):
     check(lib().rc_fill_splitmix(ptr, nbytes, seed, stream_id, hip_stream or None))
 
 
+def read_probe(ptr, nbytes, out_ptr, hip_stream=0):
+    check(lib().rc_read_probe(ptr, nbytes, out_ptr, hip_stream or None))
+
+
 def tables_key(key16, ds):
     ds = _ptr_array(ds)
     out = np.zeros(len(ds), dtype=np.uint64)

@@ -272,7 +272,10 @@ int stage_descriptors(rc_chunker *ch, Workspace &ws, uint64_t n, const uint8_t *
             const uint64_t P = open ? lens[i] : (last ? last[i] : 0);
             if (argmax_bound(ch->max_length, lens[i], P, b)) total += b;
         }
-        uint64_t seg = ch->seg_force ? ch->seg_force : std::max<uint64_t>(total / kChainWalkers, 1);
+        // a stream gets floor(bound / seg) + 1 segments: size them with headroom so that a
+        // batch of equal streams lands on one walker each when it already has enough streams
+        uint64_t seg = ch->seg_force ? ch->seg_force
+                                     : std::max<uint64_t>(total / kChainWalkers / 4 * 5 + 4, 1);
         const uint64_t floor_len = ch->max_length < (1ull << 60) ? 3 * ch->max_length : ~0ull >> 2;
         if (!ch->seg_force) seg = std::max(seg, std::max<uint64_t>(floor_len, 4ull << 20));
         seg = std::max<uint64_t>((seg + 3) & ~3ull, 4);
@@ -716,6 +719,13 @@ int rc_timing_read(rc_chunker *ch, double *phase_a_ms, double *phase_b_ms, uint6
     if (phase_b_ms) *phase_b_ms = b;
     if (calls) *calls = ch->ev_rec.size();
     ch->ev_rec.clear();
+    return RC_OK;
+}
+
+int rc_read_probe(const uint8_t *d_src, uint64_t nbytes, uint32_t *d_out, void *hip_stream) {
+    if (nbytes && (!d_src || !d_out)) return fail(RC_ERR_ARGUMENT, "null argument");
+    if (reinterpret_cast<uintptr_t>(d_src) & 15) return fail(RC_ERR_ALIGN, "source not 16-byte aligned");
+    if (rc_launch_read_probe(d_src, nbytes, d_out, hip_stream)) return fail(RC_ERR_HIP, "%s", rc_launch_error());
     return RC_OK;
 }
 

@@ -707,7 +707,7 @@ __device__ __forceinline__ uint64_t find_index(const uint64_t *base_arr, uint64_
 // Spec kernel: one wave per segment.  A one-segment stream writes its final cuts directly;
 // segment i of a longer stream writes its list to the scratch and its count (bit 63 set if the
 // chain ended inside the list: tail rule or stop).
-__global__ __launch_bounds__(256) void rc_spec_kernel(const KeyTables *__restrict__ tab,
+__global__ __launch_bounds__(512) void rc_spec_kernel(const KeyTables *__restrict__ tab,
                                                       StreamDesc d, uint64_t n_streams,
                                                       ChainParams prm, uint64_t n_segs,
                                                       const TileRecord *__restrict__ rec,
@@ -898,6 +898,43 @@ __global__ __launch_bounds__(256) void rc_join_kernel(const KeyTables *__restric
     if (lane == 0) counts[s] = overflow ? -1 : (int64_t)n;
 }
 
+// ---------------------------------------------------------------- read-bandwidth probe
+//
+// Calibration only (bench.py --calibrate): streams `nbytes` with exactly the tile kernel's
+// access pattern -- persistent 1024-thread workgroups, each wave reading 16 KiB tiles through
+// a 16-slot register ring of 16-byte nontemporal loads -- and XORs them.  Its rate is the
+// streaming-read ceiling the tile kernel is compared against on the same box.
+__global__ __launch_bounds__(1024) void rc_read_probe_kernel(const uint8_t *__restrict__ src,
+                                                             uint64_t n_tiles,
+                                                             uint32_t *__restrict__ out) {
+    const uint32_t lane = lane_id();
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t gw = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
+    const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    uint64_t t = n_tiles * gw / nw;
+    const uint64_t t_end = n_tiles * (gw + 1) / nw;
+    if (t >= t_end) return;
+    u32x4 x[kTileIters];
+    gu32x4 *p = as_global_x4(src + t * (uint64_t)kTileKeys * 4) + lane;
+#pragma unroll
+    for (int it = 0; it < kTileIters; ++it) {
+        x[it] = __builtin_nontemporal_load(p + it * 64);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    uint32_t acc = 0;
+    for (; t < t_end; ++t) {
+        const uint64_t tn = t + 1 < t_end ? t + 1 : t;
+        gu32x4 *q = as_global_x4(src + tn * (uint64_t)kTileKeys * 4) + lane;
+#pragma unroll
+        for (int it = 0; it < kTileIters; ++it) {
+            const u32x4 w = x[it];
+            acc = max3_u32(acc, w.x ^ w.y, w.z ^ w.w);
+            x[it] = __builtin_nontemporal_load(q + it * 64);
+        }
+    }
+    if (acc == 0x9E3779B9u) out[0] = acc;  // keeps the loads alive
+}
+
 // ---------------------------------------------------------------------- synthetic bytes
 
 __global__ void rc_fill_kernel(uint8_t *__restrict__ dst, uint64_t nbytes, uint64_t base) {
@@ -972,8 +1009,10 @@ int rc_launch_chain(const KeyTables *d_tables, StreamDesc desc, uint64_t n_strea
                     uint64_t *d_seg_counts, bool any_multi, void *stream) {
     if (n_streams == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
-    const uint64_t grid = (n_segs + kChainWaves - 1) / kChainWaves;
-    hipLaunchKernelGGL(rc_spec_kernel, dim3((unsigned)grid), dim3(kChainWaves * kWaveSize), 0, st,
+    // one 144 KiB-LDS workgroup per CU: 4 walkers each, 8 once there are walkers for it
+    const uint64_t wpg = n_segs >= 8 * (uint64_t)cu_count() ? 8 : kChainWaves;
+    const uint64_t grid = (n_segs + wpg - 1) / wpg;
+    hipLaunchKernelGGL(rc_spec_kernel, dim3((unsigned)grid), dim3(wpg * kWaveSize), 0, st,
                        d_tables, desc, n_streams, prm, n_segs, d_records, d_cuts, d_counts,
                        d_scratch, d_seg_counts);
     if (launch_status("rc_spec_kernel")) return 1;
@@ -983,6 +1022,17 @@ int rc_launch_chain(const KeyTables *d_tables, StreamDesc desc, uint64_t n_strea
                        d_tables, desc, n_streams, prm, d_records, d_cuts, d_counts,
                        (const uint64_t *)d_scratch, (const uint64_t *)d_seg_counts);
     return launch_status("rc_join_kernel");
+}
+
+int rc_launch_read_probe(const uint8_t *d_src, uint64_t nbytes, uint32_t *d_out, void *stream) {
+    const uint64_t n_tiles = nbytes / ((uint64_t)kTileKeys * 4);
+    if (n_tiles == 0) return 0;
+    uint64_t grid = (n_tiles + 15) / 16;
+    const uint64_t cus = (uint64_t)cu_count();
+    if (grid > cus) grid = cus;
+    hipLaunchKernelGGL(rc_read_probe_kernel, dim3((unsigned)grid), dim3(1024), 0,
+                       (hipStream_t)stream, d_src, n_tiles, d_out);
+    return launch_status("rc_read_probe_kernel");
 }
 
 int rc_launch_fill(uint8_t *d_dst, uint64_t nbytes, uint64_t seed, uint64_t stream_id,

@@ -25,7 +25,29 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
 sys.path.insert(0, os.path.dirname(HERE))
 
+def _load_reference_extension():
+    """Bind `_replicat_adapters` to the reference's own extension (oracle/_ref) before replicat
+    imports it: the repository root also holds a module of that name (the drop-in), which
+    must never stand in for the reference here."""
+    import glob
+    import importlib.machinery
+    import importlib.util
+    so = glob.glob(os.path.join(os.path.dirname(os.path.dirname(HERE)), 'oracle', '_ref',
+                                '_replicat_adapters*.so'))
+    if not so:
+        raise SystemExit('build the reference extension first: make -C oracle ref')
+    loader = importlib.machinery.ExtensionFileLoader('_replicat_adapters', so[0])
+    spec = importlib.util.spec_from_loader('_replicat_adapters', loader)
+    mod = importlib.util.module_from_spec(spec)
+    loader.exec_module(mod)
+    sys.modules['_replicat_adapters'] = mod
+    return mod
+
+
+REF_EXT = _load_reference_extension()
 from replicat.utils import adapters  # noqa: E402  (reference)
+assert adapters._replicat_adapters is REF_EXT, 'reference adapter must use the reference extension'
+
 from replicat_amd import synth  # noqa: E402
 
 MIN_DEF, MAX_DEF = 128_000, 5_120_000
@@ -248,16 +270,7 @@ from golden_surface import SURFACE_CASES, surface_call  # noqa: E402
 
 
 def make_surface():
-    # the reference's extension (oracle/_ref), loaded by path: the repository root also holds a
-    # `_replicat_adapters` (the drop-in) that must not shadow it here
-    import glob
-    import importlib.machinery
-    import importlib.util
-    so = glob.glob(os.path.join(os.path.dirname(os.path.dirname(HERE)), 'oracle', '_ref',
-                                '_replicat_adapters*.so'))[0]
-    loader = importlib.machinery.ExtensionFileLoader('_replicat_adapters', so)
-    mod = importlib.util.module_from_spec(importlib.util.spec_from_loader('_replicat_adapters', loader))
-    loader.exec_module(mod)
+    mod = REF_EXT
     out = []
     for name, args, call in SURFACE_CASES:
         try:
@@ -271,8 +284,54 @@ def make_surface():
     return out
 
 
+# ------------------------------------------------------------------ snapshots
+
+
+def snapshot_sets():
+    """File sets (name -> bytes) for snapshot framing fixtures, reproducible without the
+    reference: the reference test's own set (test_repository.py:603-620, Random(0)) and a
+    synthetic set whose files straddle the 16 MiB piece size."""
+    rnd = random.Random(0)
+    sizes = [('a', 4099), ('b', 32), ('c', 1023), ('d', 517), ('e', 2), ('f', 128), ('g', 64),
+             ('h', 2048), ('i', 19), ('j', 8), ('k', 4), ('l', 256), ('m', 1), ('n', 0),
+             ('o', 0), ('p', 19)]
+    test_set = {name: (rnd.randbytes(n) if n else b'') for name, n in sizes}
+    big = {}
+    for i, n in enumerate([0, 3, (16 << 20) - 1, (16 << 20) + 5, 7_000_001, (33 << 20) + 2]):
+        big['f%02d' % i] = synth.stream_bytes(n, synth.DEFAULT_SEED, 900 + i).tobytes() if n else b''
+    return [('reference_test_set', test_set, 256, 512, None),
+            ('reference_test_set_seeded', test_set, 256, 512, bytes(range(16))),
+            ('big_files', big, MIN_DEF, MAX_DEF, None)]
+
+
+def reference_stream_pieces(files):
+    """_stream_files (repository.py:1413-1452) over in-memory files, sorted per :1352."""
+    order = sorted(files.items(), key=lambda kv: (len(kv[1]), kv[0]))
+    prev_len = None
+    for name, data in order:
+        if prev_len is not None and -prev_len % 4:
+            yield bytes(-prev_len % 4)
+        for i in range(0, len(data), 16_777_216):
+            yield data[i:i + 16_777_216]
+        prev_len = len(data)
+
+
+def make_snapshots():
+    out = []
+    for name, files, mn, mx, params in snapshot_sets():
+        lens = ref_lengths(mn, mx, list(reference_stream_pieces(files)), params)
+        out.append({'name': name, 'min': mn, 'max': mx,
+                    'params': None if params is None else params.hex(), 'lengths': lens})
+    return out
+
+
 def main():
     quick = '--quick' in sys.argv
+    if '--snapshots-only' in sys.argv:
+        with open(os.path.join(HERE, 'snapshots.json'), 'w') as f:
+            json.dump(make_snapshots(), f, separators=(',', ':'))
+            f.write('\n')
+        return
     if '--surface-only' in sys.argv:
         with open(os.path.join(HERE, 'surface.json'), 'w') as f:
             json.dump(make_surface(), f, indent=0)
@@ -283,6 +342,7 @@ def main():
             json.dump(obj, f, separators=(',', ':'))
             f.write('\n')
     dump('surface.json', make_surface())
+    dump('snapshots.json', make_snapshots())
     dump('small_cases.json', make_small_cases())
     dump('known_answers.json', make_known_answers())
     with mp.get_context('fork').Pool(8) as pool:
