@@ -123,6 +123,25 @@ def cpu_baseline(n_streams, size, seed, procs):
                       f'{wall:.1f} s wall incl. data generation)'}, ends
 
 
+# ------------------------------------------------------------------- multi-GPU plumbing
+
+def shard_ids(config, rank, n):
+    """Stream ids a rank chunks (weak scaling: every rank has its own n streams).  Config 4
+    follows the north star's round-robin: stream i lives on GPU i mod 8."""
+    if config == '4':
+        return [rank + 8 * i for i in range(n)]
+    return [rank * n + i for i in range(n)]
+
+
+def reduce_max(values, dist, device):
+    """Max over ranks of a few floats (elapsed time, kernel times): the job is as slow as its
+    slowest rank.  The only collective the bench uses besides its barriers."""
+    import torch
+    t = torch.tensor(values, dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return t.tolist()
+
+
 # ------------------------------------------------------------------------------ main
 
 def main():
@@ -151,7 +170,7 @@ def main():
     pool = torch.empty(n * size, dtype=torch.uint8, device='cuda')  # one 16-B aligned arena
     base_ptr = pool.data_ptr()
     ptrs = [base_ptr + i * size for i in range(n)]
-    ids = [rank + 8 * i for i in range(n)] if args.config == '4' else [rank * n + i for i in range(n)]
+    ids = shard_ids(args.config, rank, n)
     for p, i in zip(ptrs, ids):
         fill_splitmix(p, size, synth.DEFAULT_SEED, i, hs)
     lens = [size] * n
@@ -181,9 +200,7 @@ def main():
     ch.timing(False)
     a_ms, b_ms, calls = ch.read_timing()
     if world > 1:
-        t = torch.tensor([elapsed, a_ms, b_ms], dtype=torch.float64, device='cuda')
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, a_ms, b_ms = t.tolist()
+        elapsed, a_ms, b_ms = reduce_max([elapsed, a_ms, b_ms], dist, 'cuda')
 
     bytes_per_step = n * size
     value = world * bytes_per_step * args.steps / elapsed / GIB
