@@ -15,7 +15,10 @@
 
 namespace rc {
 
-constexpr int kTileIters = 16;       // 16-byte loads per lane per tile (16 KiB in flight per wave)
+#ifndef RC_TILE_ITERS
+#define RC_TILE_ITERS 16
+#endif
+constexpr int kTileIters = RC_TILE_ITERS;  // 16-byte loads per lane per tile (16 KiB in flight per wave)
 constexpr int kTileKeys = 64 * 4 * kTileIters;  // keys per tile = one wave: 64 lanes x 4 keys
 constexpr int kWaveSize = 64;
 constexpr int kTileWaves = 16;       // waves per workgroup of the tile kernel (1024 threads)

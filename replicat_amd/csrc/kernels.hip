@@ -39,6 +39,12 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) const u32x4 gu32x4;
 typedef __attribute__((address_space(1))) const uint32_t gu32;
 
+#ifdef RC_PLAIN_LOADS  // diagnostic build: default cache policy for the streamed bytes
+#define RC_STREAM_LOAD(p) (*(p))
+#else
+#define RC_STREAM_LOAD(p) __builtin_nontemporal_load(p)
+#endif
+
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63; }
 
 // v_max3_u32 as an opaque step: left to itself LLVM reassociates the running maxima of the
@@ -224,7 +230,7 @@ __device__ __forceinline__ void tile_scan(const TileRef &tr, const TileRef &nx,
         pf_addrs(x[it].y, lb_a, lb_b, a + 4);
         pf_addrs(x[it].z, lb_a, lb_b, a + 8);
         pf_addrs(x[it].w, lb_a, lb_b, a + 12);
-        x[it] = __builtin_nontemporal_load(nsrc + it * 64);
+        x[it] = RC_STREAM_LOAD(nsrc + it * 64);
         const uint32_t e0 = pf_gather(a + 0);
         const uint32_t e1 = pf_gather(a + 4);
         const uint32_t e2 = pf_gather(a + 8);
@@ -349,7 +355,7 @@ __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restri
         gu32x4 *src = as_global_x4(cur.base + 4 * cur.j0) + lane;
 #pragma unroll
         for (int it = 0; it < kTileIters; ++it) {
-            x[it] = __builtin_nontemporal_load(src + it * 64);
+            x[it] = RC_STREAM_LOAD(src + it * 64);
             __builtin_amdgcn_sched_barrier(0);  // issue in ring order: the waits count on it
         }
     }
@@ -537,55 +543,72 @@ __device__ __forceinline__ ChainStream chain_stream(const StreamDesc &d, uint64_
 // lane-local key index (0-255 head, 256-511 tail; a range holds at most 8190 keys).
 constexpr int kEdgeIters = 8;  // 256-key iterations whose loads are issued together
 
-__device__ __forceinline__ void edge_prefilter(const uint8_t *base, uint64_t wmax, uint64_t a0,
-                                               uint64_t b0, uint64_t a1, uint64_t b1,
-                                               uint32_t lb_a, uint32_t lb_b, uint32_t &acc_first,
-                                               uint32_t &acc_last) {
-    const uint32_t lane = lane_id();
-    acc_first = acc_last = 0;
-#pragma unroll 1
-    for (int R = 0; R < 2; ++R) {
-        const uint64_t a = R ? a1 : a0, b = R ? b1 : b0;
-        if (a > b) continue;
-        const uint64_t q0 = a & ~3ull;                   // first word of iteration 0
-        const uint32_t nk = (uint32_t)(b - q0);          // last key offset from q0
-        const uint8_t *p = base + 4 * q0;
-        const uint32_t wlast = (uint32_t)(wmax - q0);    // last existing word, from q0
-        uint32_t carry = pf_entry(ld_u32(base + 4 * (q0 ? q0 - 1 : 0)), lb_a, lb_b);
-        for (uint32_t it0 = 0; it0 * 256 <= nk; it0 += kEdgeIters) {
-            uint32_t w[kEdgeIters][4];
+// One edge range [a, b] of keys scanned at top-16 precision in batches of kEdgeIters 256-key
+// iterations: load() issues a batch's words, compute() folds them into the lane's running
+// maxima.  Splitting the two lets a chain step put the record loads and both ranges' first
+// batches in flight together (one memory round trip for a typical step).
+struct EdgeRange {
+    const uint8_t *p;     // word q0 of the stream
+    uint64_t a, q0;       // first key, first word of iteration 0 (a & ~3)
+    uint32_t nk, wlast;   // last key offset from q0, last existing word from q0
+    uint32_t it0;         // next iteration to load
+    uint32_t carry;       // entry of the word before the next iteration's lane 0 key
+    uint32_t carry_word;
+    uint32_t R;           // 0 head / 1 tail (lane-local order 256*R + 4*it + k)
+    bool live;
+
+    __device__ void init(const uint8_t *base, uint64_t wmax, uint64_t a_, uint64_t b_, uint32_t R_) {
+        R = R_;
+        live = a_ <= b_;
+        a = a_;
+        q0 = a_ & ~3ull;
+        nk = live ? (uint32_t)(b_ - q0) : 0;
+        p = base + 4 * q0;
+        wlast = live ? (uint32_t)(wmax - q0) : 0;
+        it0 = 0;
+        carry_word = live ? ld_u32(base + 4 * (q0 ? q0 - 1 : 0)) : 0;
+        carry = 0;
+    }
+    __device__ bool more() const { return live && it0 * 256 <= nk; }
+    __device__ void load(uint32_t (&w)[kEdgeIters][4]) const {
+        const uint32_t lane = lane_id();
 #pragma unroll
-            for (int i = 0; i < kEdgeIters; ++i)
+        for (int i = 0; i < kEdgeIters; ++i)
 #pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    w[i][k] = ld_u32(p + 4 * min((it0 + i) * 256 + lane * 4 + k, wlast));
+            for (int k = 0; k < 4; ++k)
+                w[i][k] = ld_u32(p + 4 * min((it0 + i) * 256 + lane * 4 + k, wlast));
+    }
+    __device__ void compute(const uint32_t (&w)[kEdgeIters][4], uint32_t lb_a, uint32_t lb_b,
+                            uint32_t &acc_first, uint32_t &acc_last) {
+        const uint32_t lane = lane_id();
+        if (it0 == 0) carry = pf_entry(carry_word, lb_a, lb_b);
 #pragma unroll
-            for (int i = 0; i < kEdgeIters; ++i) {
-                const uint32_t it = it0 + i;
-                uint32_t ad[16];
-                pf_addrs(w[i][0], lb_a, lb_b, ad + 0);
-                pf_addrs(w[i][1], lb_a, lb_b, ad + 4);
-                pf_addrs(w[i][2], lb_a, lb_b, ad + 8);
-                pf_addrs(w[i][3], lb_a, lb_b, ad + 12);
-                const uint32_t e0 = pf_gather(ad + 0), e1 = pf_gather(ad + 4);
-                const uint32_t e2 = pf_gather(ad + 8), e3 = pf_gather(ad + 12);
-                const uint32_t rot = __builtin_amdgcn_update_dpp(0u, e3, 0x13C, 0xf, 0xf, false);
-                const uint32_t ep = lane == 0 ? carry : rot;
-                carry = rot;
-                const uint32_t t[4] = {(ep & 0xffff0000u) ^ (e0 << 16), (e0 & 0xffff0000u) ^ (e1 << 16),
-                                       (e1 & 0xffff0000u) ^ (e2 << 16), (e2 & 0xffff0000u) ^ (e3 << 16)};
+        for (int i = 0; i < kEdgeIters; ++i) {
+            const uint32_t it = it0 + i;
+            uint32_t ad[16];
+            pf_addrs(w[i][0], lb_a, lb_b, ad + 0);
+            pf_addrs(w[i][1], lb_a, lb_b, ad + 4);
+            pf_addrs(w[i][2], lb_a, lb_b, ad + 8);
+            pf_addrs(w[i][3], lb_a, lb_b, ad + 12);
+            const uint32_t e0 = pf_gather(ad + 0), e1 = pf_gather(ad + 4);
+            const uint32_t e2 = pf_gather(ad + 8), e3 = pf_gather(ad + 12);
+            const uint32_t rot = __builtin_amdgcn_update_dpp(0u, e3, 0x13C, 0xf, 0xf, false);
+            const uint32_t ep = lane == 0 ? carry : rot;
+            carry = rot;
+            const uint32_t t[4] = {(ep & 0xffff0000u) ^ (e0 << 16), (e0 & 0xffff0000u) ^ (e1 << 16),
+                                   (e1 & 0xffff0000u) ^ (e2 << 16), (e2 & 0xffff0000u) ^ (e3 << 16)};
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const uint32_t off = it * 256 + lane * 4 + k;   // key q0 + off
-                    const bool valid = off <= nk && q0 + off >= a;
-                    const uint32_t local = 256u * R + it * 4 + k;
-                    acc_first = max3_u32(acc_first, valid ? (t[k] | 0x8000u | (511u - local)) : 0u, 0u);
-                    acc_last = max3_u32(acc_last, valid ? (t[k] | 0x8000u | local) : 0u, 0u);
-                }
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t off = it * 256 + lane * 4 + k;  // key q0 + off
+                const bool valid = off <= nk && q0 + off >= a;
+                const uint32_t local = 256u * R + it * 4 + k;
+                acc_first = max3_u32(acc_first, valid ? (t[k] | 0x8000u | (511u - local)) : 0u, 0u);
+                acc_last = max3_u32(acc_last, valid ? (t[k] | 0x8000u | local) : 0u, 0u);
             }
         }
+        it0 += kEdgeIters;
     }
-}
+};
 
 enum : int { kStepStop = 0, kStepCut = 1, kStepTail1 = 2, kStepTail2 = 3 };
 
@@ -629,20 +652,44 @@ __device__ int chain_step(const uint64_t *tl, const uint64_t *th, const TileReco
             const uint64_t t_lo = (ja + kTileKeys - 1) / kTileKeys;
             const uint64_t t_hi = (jb + 1) / kTileKeys;
             uint64_t a0 = ja, b0 = jb, a1 = 1, b1 = 0;
-            if (t_lo < t_hi) {
-#ifndef RC_DIAG_SKIP_RECORDS
-                scan_records(rec, st.tb0 + t_lo, st.tb0 + t_hi, bk, bj);
-#endif
+            const bool have_rec = t_lo < t_hi;
+            if (have_rec) {
                 b0 = t_lo * kTileKeys - 1;
                 a1 = t_hi * kTileKeys;
                 b1 = jb;
             }
+            // one round trip: the records and both edge ranges' first batches in flight
+            EdgeRange r0, r1;
+            r0.init(st.base, st.L / 4 - 1, a0, b0, 0);
+            r1.init(st.base, st.L / 4 - 1, a1, b1, 1);
+            uint32_t w0[kEdgeIters][4], w1[kEdgeIters][4];
+            uint32_t acc_first = 0, acc_last = 0;
+            TileRecord rv[kRecUnroll];
+            const uint64_t rlo = st.tb0 + t_lo, rhi = st.tb0 + t_hi;
+            if (have_rec) {
+#pragma unroll
+                for (int u = 0; u < kRecUnroll; ++u) rv[u] = rec[min(rlo + 64 * u + lane_id(), rhi - 1)];
+            }
+            if (r0.more()) r0.load(w0);
+            if (r1.more()) r1.load(w1);
+            if (have_rec) {
+#pragma unroll
+                for (int u = 0; u < kRecUnroll; ++u)
+                    if (rlo + 64 * u + lane_id() < rhi && rv[u].key != 0)
+                        take_best(rv[u].key, rv[u].j, bk, bj);
+                if (rhi - rlo > 64 * kRecUnroll)  // windows beyond 512 tiles (max > 8 MiB)
+                    scan_records(rec, rlo + 64 * kRecUnroll, rhi, bk, bj);
+            }
             wave_best(bk, bj);
             RC_STAMP(2);
-            uint32_t acc_first = 0, acc_last = 0;
-#ifndef RC_DIAG_SKIP_EDGES
-            edge_prefilter(st.base, st.L / 4 - 1, a0, b0, a1, b1, lb_a, lb_b, acc_first, acc_last);
-#endif
+            for (;;) {
+                const bool m0 = r0.more(), m1 = r1.more();
+                if (!m0 && !m1) break;
+                if (m0) r0.compute(w0, lb_a, lb_b, acc_first, acc_last);
+                if (m1) r1.compute(w1, lb_a, lb_b, acc_first, acc_last);
+                if (r0.more()) r0.load(w0);
+                if (r1.more()) r1.load(w1);
+            }
             RC_STAMP(3);
             const uint32_t m = wave_max_u32(acc_first);
             if ((m & 0x8000u) && (m >> 16) >= (uint32_t)(bk >> 48)) {
@@ -918,7 +965,7 @@ __global__ __launch_bounds__(1024) void rc_read_probe_kernel(const uint8_t *__re
     gu32x4 *p = as_global_x4(src + t * (uint64_t)kTileKeys * 4) + lane;
 #pragma unroll
     for (int it = 0; it < kTileIters; ++it) {
-        x[it] = __builtin_nontemporal_load(p + it * 64);
+        x[it] = RC_STREAM_LOAD(p + it * 64);
         __builtin_amdgcn_sched_barrier(0);
     }
     uint32_t acc = 0;
@@ -929,7 +976,7 @@ __global__ __launch_bounds__(1024) void rc_read_probe_kernel(const uint8_t *__re
         for (int it = 0; it < kTileIters; ++it) {
             const u32x4 w = x[it];
             acc = max3_u32(acc, w.x ^ w.y, w.z ^ w.w);
-            x[it] = __builtin_nontemporal_load(q + it * 64);
+            x[it] = RC_STREAM_LOAD(q + it * 64);
         }
     }
     if (acc == 0x9E3779B9u) out[0] = acc;  // keeps the loads alive
