@@ -231,10 +231,14 @@ __device__ __forceinline__ void tile_scan(const TileRef &tr, const TileRef &nx,
         pf_addrs(x[it].z, lb_a, lb_b, a + 8);
         pf_addrs(x[it].w, lb_a, lb_b, a + 12);
         x[it] = RC_STREAM_LOAD(nsrc + it * 64);
+#ifdef RC_DIAG_NO_LOOKUPS  // diagnostic build: no table reads (cost split)
+        const uint32_t e0 = a[0] ^ a[1], e1 = a[4] ^ a[5], e2 = a[8] ^ a[9], e3 = a[12] ^ a[13];
+#else
         const uint32_t e0 = pf_gather(a + 0);
         const uint32_t e1 = pf_gather(a + 4);
         const uint32_t e2 = pf_gather(a + 8);
         const uint32_t e3 = pf_gather(a + 12);
+#endif
         // previous word's entry for key 0 of this lane: lane-1's e3 (wave_ror:1); lane 0 takes
         // the carry = lane 63's e3 of the previous iteration (or the word before the tile).
         const uint32_t rot = __builtin_amdgcn_update_dpp(0u, e3, 0x13C, 0xf, 0xf, false);
@@ -380,6 +384,7 @@ __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restri
         tile_scan(cur, nx, x, prev_word, lb_a, lb_b, top, first, last);
 
         // retire the pending tile: (first maximal exact key, index) over its candidate lanes
+#ifndef RC_DIAG_NO_TAIL
         {
             const uint64_t k = full_key(tl, th, pend_lo, pend_hi);
             uint64_t bk = 0, bj = kTieMark;
@@ -415,6 +420,9 @@ __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restri
         const uint8_t *q = cur.base + 4 * (cur.j0 + pend_jl);
         pend_lo = ld_u32(q - 4);
         pend_hi = ld_u32(q);
+#else
+        if (lane == 0 && (top ^ first ^ last) == 0x5a5au) rec[t].key = first ^ last;  // keep the scan alive
+#endif
 
         if (!nx.fast) break;
         t = tn;
