@@ -41,9 +41,22 @@ typedef __attribute__((address_space(1))) const uint32_t gu32;
 
 #ifdef RC_PLAIN_LOADS  // diagnostic build: default cache policy for the streamed bytes
 #define RC_STREAM_LOAD(p) (*(p))
+constexpr int kStreamAux = 0;
 #else
 #define RC_STREAM_LOAD(p) __builtin_nontemporal_load(p)
+constexpr int kStreamAux = 2;  // nt
 #endif
+
+// The tile ring reads through a buffer resource based at the tile: the lane offset stays in one
+// VGPR for the whole kernel and the slot offset is an SGPR, so a reissue costs no address VALU
+// (a 64-bit global address would need a v_add_co/v_addc pair per 4 KiB of immediate range).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const uint8_t *base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(base), 0, 0xffffffffu,
+                                             0x00020000);
+}
+__device__ __forceinline__ u32x4 ring_load(__amdgpu_buffer_rsrc_t r, uint32_t lane_off, int it) {
+    return __builtin_amdgcn_raw_buffer_load_b128(r, lane_off, it * 1024, kStreamAux);
+}
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63; }
 
@@ -217,7 +230,7 @@ __device__ __forceinline__ void tile_scan(const TileRef &tr, const TileRef &nx,
     // no next fast tile (end of the wave's range): harmlessly re-read this tile instead, so
     // the ring loads stay unconditional
     const uint8_t *nbase = nx.fast ? nx.base + 4 * nx.j0 : tr.base + 4 * tr.j0;
-    gu32x4 *nsrc = as_global_x4(nbase) + lane;
+    const __amdgpu_buffer_rsrc_t nsrc = tile_rsrc(nbase);
     uint32_t carry = pf_entry(prev_word, lb_a, lb_b);
     prev_word = ld_u32(nbase - 4);
     uint32_t acc_first = 0, acc_last = 0;
@@ -230,7 +243,7 @@ __device__ __forceinline__ void tile_scan(const TileRef &tr, const TileRef &nx,
         pf_addrs(x[it].y, lb_a, lb_b, a + 4);
         pf_addrs(x[it].z, lb_a, lb_b, a + 8);
         pf_addrs(x[it].w, lb_a, lb_b, a + 12);
-        x[it] = RC_STREAM_LOAD(nsrc + it * 64);
+        x[it] = ring_load(nsrc, lane * 16, it);
 #ifdef RC_DIAG_NO_LOOKUPS  // diagnostic build: no table reads (cost split)
         const uint32_t e0 = a[0] ^ a[1], e1 = a[4] ^ a[5], e2 = a[8] ^ a[9], e3 = a[12] ^ a[13];
 #else
@@ -241,7 +254,7 @@ __device__ __forceinline__ void tile_scan(const TileRef &tr, const TileRef &nx,
 #endif
         // previous word's entry for key 0 of this lane: lane-1's e3 (wave_ror:1); lane 0 takes
         // the carry = lane 63's e3 of the previous iteration (or the word before the tile).
-        const uint32_t rot = __builtin_amdgcn_update_dpp(0u, e3, 0x13C, 0xf, 0xf, false);
+        const uint32_t rot = __builtin_amdgcn_mov_dpp(e3, 0x13C, 0xf, 0xf, false);
         const uint32_t ep = lane == 0 ? carry : rot;
         carry = rot;
         const uint32_t b0 = (ep & 0xffff0000u) ^ (e0 << 16);
@@ -356,10 +369,10 @@ __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restri
     u32x4 x[kTileIters];
     uint32_t prev_word = ld_u32(cur.base + 4 * cur.j0 - 4);
     {
-        gu32x4 *src = as_global_x4(cur.base + 4 * cur.j0) + lane;
+        const __amdgpu_buffer_rsrc_t src = tile_rsrc(cur.base + 4 * cur.j0);
 #pragma unroll
         for (int it = 0; it < kTileIters; ++it) {
-            x[it] = RC_STREAM_LOAD(src + it * 64);
+            x[it] = ring_load(src, lane * 16, it);
             __builtin_amdgcn_sched_barrier(0);  // issue in ring order: the waits count on it
         }
     }
@@ -600,7 +613,7 @@ struct EdgeRange {
             pf_addrs(w[i][3], lb_a, lb_b, ad + 12);
             const uint32_t e0 = pf_gather(ad + 0), e1 = pf_gather(ad + 4);
             const uint32_t e2 = pf_gather(ad + 8), e3 = pf_gather(ad + 12);
-            const uint32_t rot = __builtin_amdgcn_update_dpp(0u, e3, 0x13C, 0xf, 0xf, false);
+            const uint32_t rot = __builtin_amdgcn_mov_dpp(e3, 0x13C, 0xf, 0xf, false);
             const uint32_t ep = lane == 0 ? carry : rot;
             carry = rot;
             const uint32_t t[4] = {(ep & 0xffff0000u) ^ (e0 << 16), (e0 & 0xffff0000u) ^ (e1 << 16),
