@@ -34,10 +34,13 @@ def parse():
     p.add_argument('--gpus', type=int, default=1)
     p.add_argument('--steps', type=int, default=10)
     p.add_argument('--warmup', type=int, default=2)
-    p.add_argument('--config', choices=['2', '3i', '3iii', '4'], default='2',
+    p.add_argument('--config', choices=['2', '3i', '3ii', '3iii', '4', '5'], default='2',
                    help='2: 1024 x 64 MiB (the metric); 3i: 65536 x 1 MiB default params '
-                        '(degenerate: tail rule only); 3iii: 65536 x 1 MiB, min 2000 / max 80000; '
-                        '4: 16 x 8 GiB per GPU (streams rank, rank+8, ...)')
+                        '(degenerate: tail rule only); 3ii: ONE 64 GiB stream, last piece the '
+                        'final 1 MiB (snapshot framing, segment-parallel chain); 3iii: 65536 x '
+                        '1 MiB, min 2000 / max 80000; 4: 16 x 8 GiB per GPU (streams rank, '
+                        'rank+8, ...); 5: re-chunk of config 2 with 512 edited copies + dedup '
+                        'ratio check')
     p.add_argument('--streams', type=int, default=None)
     p.add_argument('--stream-mib', type=int, default=None)
     p.add_argument('--calibrate', action='store_true',
@@ -142,6 +145,148 @@ def reduce_max(values, dist, device):
     return t.tolist()
 
 
+# ------------------------------------------------------------------- config 5 (dedup)
+
+class Config5:
+    """config 2's streams, of which 512 (synth.edit_plan) get one edit
+    each; the edited set is re-chunked and its dedup ratio against the original set computed.
+
+    Content identity on the device: an edited-set chunk can only equal an original chunk of the
+    same stream at the same bytes -- before the edit at the same offsets, after it shifted by the
+    insert length -- so those candidates are looked up by offset and confirmed by comparing the
+    bytes in HBM (torch.equal).  The reference value (tests/golden/large.json) looks every chunk
+    up by BLAKE2b-512 content digest over the whole original set instead, so the two agree only
+    if no other coincidence exists."""
+
+    def __init__(self, ch, pool, slot, n, size, rank, hs):
+        import torch
+        from replicat_amd import synth
+        self.size, self.slot, self.n = size, slot, n
+        self.orig = pool
+        base = pool.data_ptr()
+        olens = [size] * n
+        cap, ocaps = ch.capacity(olens)
+        ocuts = torch.zeros(cap, dtype=torch.int64, device='cuda')
+        ocounts = torch.zeros(n, dtype=torch.int64, device='cuda')
+        ch.chunk_device([base + i * slot for i in range(n)], olens, None, ocuts.data_ptr(),
+                        ocounts.data_ptr(), hs)
+        self.orig_digest, _, self.orig_ends = cut_digest(ocuts, ocounts, ocaps)
+        plan = synth.edit_plan(n, n // 2, size) if rank == 0 and n == 1024 else []
+        self.plan = {sid: (kind, off, payload) for sid, kind, off, payload in plan}
+        self.edited = sorted(self.plan)
+        self.buf = torch.empty(n * slot + 64, dtype=torch.uint8, device='cuda')
+        self.lens = []
+        for i in range(n):
+            src = pool[i * slot:i * slot + size]
+            dst = self.buf[i * slot:]
+            kind, off, payload = self.plan.get(i, (None, 0, b''))
+            if kind is None:
+                dst[:size].copy_(src)
+            elif kind == 'overwrite1':
+                dst[:size].copy_(src)
+                dst[off:off + 1] ^= 0x5A
+            else:
+                k = len(payload)
+                dst[:off].copy_(src[:off])
+                dst[off:off + k].copy_(torch.tensor(list(payload), dtype=torch.uint8))
+                dst[off + k:size + k].copy_(src[off:])
+            self.lens.append(size + len(payload))
+        self.ptrs = [self.buf.data_ptr() + i * slot for i in range(n)]
+
+    def dedup(self, ends):
+        """Dedup bytes of the edited streams (integers, comparable with the reference's)."""
+        dup = total = 0
+        for sid in self.edited:
+            kind, off, payload = self.plan[sid]
+            d = len(payload)
+            lo_end = off            # a chunk ending at or before this is untouched
+            hi_start = off + max(d, 1)  # a chunk starting here or later is shifted by d
+            orig = self.orig_ends[sid]
+            ostarts, prev = {}, 0
+            for e in orig:
+                ostarts[prev] = int(e)
+                prev = int(e)
+            a = 0
+            for e in ends[sid]:
+                e = int(e)
+                if e <= lo_end:
+                    oa, ob = a, e
+                elif a >= hi_start:
+                    oa, ob = a - d, e - d
+                else:
+                    oa = ob = None
+                if oa is not None and ostarts.get(oa) == ob:
+                    x = self.orig[sid * self.slot + oa:sid * self.slot + ob]
+                    y = self.buf[sid * self.slot + a:sid * self.slot + e]
+                    if bool((x == y).all()):
+                        dup += e - a
+                a = e
+            total += a
+        return {'dup_bytes_edited': dup, 'total_bytes_edited': total,
+                'dedup_ratio_edited': round(dup / total, 6) if total else None}
+
+
+# -------------------------------------------------------- config 3 (ii): one long stream
+
+class Config3ii:
+    """ONE stream of world x 64 GiB (last piece = the final 1 MiB) split over the ranks
+    (replicat_amd/split.py): each rank fills and chunks its window (segment + halo) with a
+    speculative chain, the ranks exchange their cut lists through a host-side (gloo) gather and
+    splice them.  One rank: the plain single-stream path (segment-parallel chain on one GPU)."""
+
+    def __init__(self, ch, size, rank, world, hs, dist):
+        import torch
+        from replicat_amd import split, synth
+        from replicat_amd.chunker import fill_splitmix_at
+        self.ch, self.rank, self.world, self.hs = ch, rank, world, hs
+        self.L = size * world
+        self.P = self.L - (1 << 20)
+        self.windows = split.plan_windows(self.L, self.P, world, ch.max_length)
+        w = self.windows[rank]
+        self.w = w
+        self.buf = torch.empty(w.end - w.start + 64, dtype=torch.uint8, device='cuda')
+        fill_splitmix_at(self.buf.data_ptr(), w.end - w.start, synth.DEFAULT_SEED, 0,
+                         w.start // 8, hs)
+        self.lens = [w.end - w.start]
+        _, caps = ch.capacity(self.lens)
+        self.cap = int(caps[0])
+        self.cuts = torch.zeros(self.cap + 1, dtype=torch.int64, device='cuda')
+        self.counts = torch.zeros(1, dtype=torch.int64, device='cuda')
+        self.group = dist.new_group(backend='gloo') if world > 1 else None
+        self.dist = dist
+        self.ends = None
+        self.rounds = 0
+
+    def chunk_window(self, w, entry):
+        import torch
+        off = entry - w.start
+        src, n = self.buf.data_ptr() + off, w.end - entry
+        tmp = None
+        if src % 16:  # a fallback entry (rare): re-base the bytes on an aligned buffer
+            tmp = torch.empty(n + 64, dtype=torch.uint8, device='cuda')
+            tmp[:n].copy_(self.buf[off:off + n])
+            src = tmp.data_ptr()
+        _, caps = self.ch.capacity([n])
+        cuts = self.cuts if int(caps[0]) <= self.cap else \
+            torch.zeros(int(caps[0]), dtype=torch.int64, device='cuda')
+        self.ch.chunk_device([src], [n], [max(0, w.last_piece - off) if not w.open else 0],
+                             cuts.data_ptr(), self.counts.data_ptr(), self.hs, open_=w.open)
+        c = int(self.counts.item())
+        return (cuts[:c].cpu().numpy() + entry).tolist()
+
+    def gather(self, obj):
+        if self.world == 1:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj, group=self.group)
+        return out
+
+    def step(self):
+        from replicat_amd import split
+        self.ends, self.rounds = split.chunk_split(self.chunk_window, self.windows, self.rank,
+                                                   self.gather)
+
+
 # ------------------------------------------------------------------------------ main
 
 def main():
@@ -160,27 +305,43 @@ def main():
     from replicat_amd.chunker import GpuChunker, fill_splitmix, read_probe
     key = b'\xff' * 16 if args.key == 'ff' else synth.seeded_key(1)
     cfg = {'2': (1024, 64, MIN_LEN, MAX_LEN), '3i': (65536, 1, MIN_LEN, MAX_LEN),
-           '3iii': (65536, 1, 2_000, 80_000), '4': (16, 8192, MIN_LEN, MAX_LEN)}[args.config]
+           '3ii': (1, 64 << 10, MIN_LEN, MAX_LEN), '3iii': (65536, 1, 2_000, 80_000),
+           '4': (16, 8192, MIN_LEN, MAX_LEN), '5': (1024, 64, MIN_LEN, MAX_LEN)}[args.config]
     n = args.streams or cfg[0]
     size = (args.stream_mib or cfg[1]) << 20
     min_len, max_len = cfg[2], cfg[3]
     ch = GpuChunker(min_len, max_len, key, device=local)
     stream = torch.cuda.current_stream()
     hs = stream.cuda_stream
-    pool = torch.empty(n * size, dtype=torch.uint8, device='cuda')  # one 16-B aligned arena
-    base_ptr = pool.data_ptr()
-    ptrs = [base_ptr + i * size for i in range(n)]
-    ids = shard_ids(args.config, rank, n)
-    for p, i in zip(ptrs, ids):
-        fill_splitmix(p, size, synth.DEFAULT_SEED, i, hs)
-    lens = [size] * n
+    last = None
+    edit = long = None
+    if args.config == '3ii':
+        long = Config3ii(ch, size, rank, world, hs, dist)
+        n, lens = 1, long.lens
+        base_ptr = long.buf.data_ptr()
+    else:
+        # stream slots 64-B aligned; config 5's inserts grow a stream by up to 4 bytes
+        slot = (size + (64 if args.config == '5' else 0) + 63) // 64 * 64
+        pool = torch.empty(n * slot + 64, dtype=torch.uint8, device='cuda')  # one arena
+        base_ptr = pool.data_ptr()
+        ptrs = [base_ptr + i * slot for i in range(n)]
+        for p, i in zip(ptrs, shard_ids(args.config, rank, n)):
+            fill_splitmix(p, size, synth.DEFAULT_SEED, i, hs)
+        lens = [size] * n
+        if args.config == '5':
+            # the original set is chunked once (untimed); the step re-chunks the edited set
+            edit = Config5(ch, pool, slot, n, size, rank, hs)
+            ptrs, lens = edit.ptrs, edit.lens
     total_cap, caps = ch.capacity(lens)
     cuts = torch.zeros(total_cap, dtype=torch.int64, device='cuda')
     counts = torch.zeros(n, dtype=torch.int64, device='cuda')
     torch.cuda.synchronize()
 
     def step():
-        ch.chunk_device(ptrs, lens, None, cuts.data_ptr(), counts.data_ptr(), hs)
+        if long is not None:
+            long.step()
+        else:
+            ch.chunk_device(ptrs, lens, last, cuts.data_ptr(), counts.data_ptr(), hs)
 
     for _ in range(args.warmup):
         step()
@@ -202,7 +363,7 @@ def main():
     if world > 1:
         elapsed, a_ms, b_ms = reduce_max([elapsed, a_ms, b_ms], dist, 'cuda')
 
-    bytes_per_step = n * size
+    bytes_per_step = sum(lens) if long is None else long.L // world
     value = world * bytes_per_step * args.steps / elapsed / GIB
     ms_per_step = elapsed * 1e3 / args.steps
     a_avg = a_ms / max(calls, 1)
@@ -212,17 +373,41 @@ def main():
     parity = None
     ends = None
     if not args.no_verify and rank == 0:
-        digest, nchunks, ends = cut_digest(cuts, counts, caps)
         sys.path.insert(0, os.path.join(ROOT, 'tests'))
         import golden_util as G
+        if long is not None:
+            ends = [np.asarray(long.ends, dtype=np.uint64)]
+            digest = G.cutlist_digest(ends)
+        else:
+            digest, nchunks, ends = cut_digest(cuts, counts, caps)
         gold = {d['name']: d for d in G.load('digests.json')}
         if args.key == 'ff' and n == 1024 and size == 64 << 20 and args.config == '2':
             parity = digest == gold['config2_ff']['sha256']
         elif args.key == 'ff' and args.config == '3iii' and n >= 4096:
             parity = G.cutlist_digest(ends[:4096]) == gold['config3iii_first4096']['sha256']
+        elif args.key == 'ff' and long is not None and long.L == 64 << 30:
+            large = {d['name']: d for d in G.load('large.json')}
+            parity = digest == large['config3ii']['sha256']
+        elif edit is not None and args.key == 'ff' and n == 1024 and size == 64 << 20:
+            large = {d['name']: d for d in G.load('large.json')}
+            dedup = edit.result = edit.dedup(ends)
+            g5 = large['config5']
+            parity = (G.cutlist_digest([ends[i] for i in edit.edited]) == g5['edited_sha256']
+                      and edit.orig_digest == g5['original_sha256']
+                      and dedup['dup_bytes_edited'] == g5['dup_bytes_edited']
+                      and dedup['total_bytes_edited'] == g5['total_bytes_edited'])
     if world > 1:
         dist.barrier()
 
+    if long is not None:
+        workload = ('config3ii: ONE stream of %d GiB (last piece = final 1 MiB) split over %d '
+                    'rank(s), min %d, max %d, key %s' % (long.L >> 30, world, min_len, max_len,
+                                                         args.key))
+    else:
+        workload = ('config%s: %d x %d MiB streams per GPU, min %d, max %d, key %s'
+                    % (args.config, n, size >> 20, min_len, max_len, args.key))
+        if edit is not None:
+            workload += ' (512 of the 1024 edited, re-chunk + dedup check)'
     result = None
     if rank == 0:
         cpu = None
@@ -234,7 +419,7 @@ def main():
                            for i in cpu_ends)
                 cpu['matches_gpu'] = bool(same)
         e2e = None
-        if args.e2e:  # host-resident streams: copies in, chunking, cut offsets out
+        if args.e2e and long is None:  # host-resident streams: copies in, chunking, cut offsets out
             m = min(n, 64)
             hbufs = [synth.stream_bytes(size, synth.DEFAULT_SEED, i) for i in range(m)]
             pinned = torch.empty(m * size, dtype=torch.uint8).pin_memory()
@@ -253,14 +438,15 @@ def main():
         if args.calibrate:
             out = torch.zeros(4, dtype=torch.int32, device='cuda')
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            probe = sum(lens) // 16 * 16
             for _ in range(2):
-                read_probe(base_ptr, n * size, out.data_ptr(), hs)
+                read_probe(base_ptr, probe, out.data_ptr(), hs)
             ev0.record(stream)
             for _ in range(5):
-                read_probe(base_ptr, n * size, out.data_ptr(), hs)
+                read_probe(base_ptr, probe, out.data_ptr(), hs)
             ev1.record(stream)
             torch.cuda.synchronize()
-            calib = round(5 * n * size / (ev0.elapsed_time(ev1) * 1e-3) / 1e9, 1)
+            calib = round(5 * probe / (ev0.elapsed_time(ev1) * 1e-3) / 1e9, 1)
         result = {
             'metric': 'GiB/s chunked, device-resident streams',
             'value': round(value, 2),
@@ -274,8 +460,7 @@ def main():
             'vs_baseline': None,
             'dtype': 'u8',
             'data': 'synthetic (splitmix64 counter streams generated in HBM)',
-            'config': {'workload': 'config%s: %d x %d MiB streams per GPU, min %d, max %d, key %s'
-                                   % (args.config, n, size >> 20, min_len, max_len, args.key),
+            'config': {'workload': workload,
                        'streams_per_gpu': n, 'stream_bytes': size, 'parallelism': f'streams/{world} ranks'},
             'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
                          'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4),
@@ -284,6 +469,8 @@ def main():
             'cpu_baseline': cpu,
             'parity_sha256': parity,
         }
+        if edit is not None and getattr(edit, 'result', None) is not None:
+            result['dedup'] = edit.result
         if calib is not None:
             result['read_probe_gbs'] = calib
         if e2e is not None:

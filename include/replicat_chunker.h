@@ -107,6 +107,10 @@ int rc_timing_read(rc_chunker *ch, double *phase_a_ms, double *phase_b_ms, uint6
  * is splitmix64((seed * 0x9E3779B97F4A7C15) ^ (stream << 34) ^ i), little-endian. */
 int rc_fill_splitmix(uint8_t *d_dst, uint64_t nbytes, uint64_t seed, uint64_t stream,
                      void *hip_stream);
+/* The same bytes from word `word0` of the stream on (byte offset 8 * word0): one segment of a
+ * long stream (the multi-device split of a single stream, replicat_amd/split.py). */
+int rc_fill_splitmix_at(uint8_t *d_dst, uint64_t nbytes, uint64_t seed, uint64_t stream,
+                        uint64_t word0, void *hip_stream);
 
 /* Calibration (bench.py --calibrate): stream the first nbytes (whole 16 KiB tiles) of a
  * 16-byte aligned device buffer with the tile kernel's exact load pattern and no hashing; its

@@ -40,6 +40,7 @@ SIGNATURES = {
     'rc_timing_read': (_int, [_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                               ctypes.POINTER(_u64)]),
     'rc_fill_splitmix': (_int, [_p, _u64, _u64, _u64, _p]),
+    'rc_fill_splitmix_at': (_int, [_p, _u64, _u64, _u64, _u64, _p]),
     'rc_read_probe': (_int, [_p, _u64, _p, _p]),
     'rc_keys_needed': (_u64, [_u64, _u64, _u64]),
     'rc_host_key': (_u64, [_p, _u64]),

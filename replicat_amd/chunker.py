@@ -144,6 +144,10 @@ def fill_splitmix(ptr, nbytes, seed, stream_id, hip_stream=0):
     check(lib().rc_fill_splitmix(ptr, nbytes, seed, stream_id, hip_stream or None))
 
 
+def fill_splitmix_at(ptr, nbytes, seed, stream_id, word0, hip_stream=0):
+    check(lib().rc_fill_splitmix_at(ptr, nbytes, seed, stream_id, word0, hip_stream or None))
+
+
 def read_probe(ptr, nbytes, out_ptr, hip_stream=0):
     check(lib().rc_read_probe(ptr, nbytes, out_ptr, hip_stream or None))
 

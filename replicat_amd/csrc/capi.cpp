@@ -731,7 +731,14 @@ int rc_read_probe(const uint8_t *d_src, uint64_t nbytes, uint32_t *d_out, void *
 
 int rc_fill_splitmix(uint8_t *d_dst, uint64_t nbytes, uint64_t seed, uint64_t stream, void *hip_stream) {
     if (nbytes && !d_dst) return fail(RC_ERR_ARGUMENT, "null destination");
-    if (rc_launch_fill(d_dst, nbytes, seed, stream, hip_stream)) return fail(RC_ERR_HIP, "%s", rc_launch_error());
+    if (rc_launch_fill(d_dst, nbytes, seed, stream, 0, hip_stream)) return fail(RC_ERR_HIP, "%s", rc_launch_error());
+    return RC_OK;
+}
+
+int rc_fill_splitmix_at(uint8_t *d_dst, uint64_t nbytes, uint64_t seed, uint64_t stream,
+                        uint64_t word0, void *hip_stream) {
+    if (nbytes && !d_dst) return fail(RC_ERR_ARGUMENT, "null destination");
+    if (rc_launch_fill(d_dst, nbytes, seed, stream, word0, hip_stream)) return fail(RC_ERR_HIP, "%s", rc_launch_error());
     return RC_OK;
 }
 

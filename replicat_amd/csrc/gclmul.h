@@ -91,7 +91,7 @@ int rc_launch_chain(const rc::KeyTables *d_tables, rc::StreamDesc desc, uint64_t
                     uint64_t *d_cuts, int64_t *d_counts, uint64_t *d_scratch,
                     uint64_t *d_seg_counts, bool any_multi, void *stream);
 int rc_launch_fill(uint8_t *d_dst, uint64_t nbytes, uint64_t seed, uint64_t stream_id,
-                   void *stream);
+                   uint64_t word0, void *stream);
 int rc_launch_read_probe(const uint8_t *d_src, uint64_t nbytes, uint32_t *d_out, void *stream);
 const char *rc_launch_error(void);
 }

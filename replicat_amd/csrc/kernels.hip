@@ -1005,14 +1005,15 @@ __global__ __launch_bounds__(1024) void rc_read_probe_kernel(const uint8_t *__re
 
 // ---------------------------------------------------------------------- synthetic bytes
 
-__global__ void rc_fill_kernel(uint8_t *__restrict__ dst, uint64_t nbytes, uint64_t base) {
+__global__ void rc_fill_kernel(uint8_t *__restrict__ dst, uint64_t nbytes, uint64_t base,
+                               uint64_t word0) {
     const uint64_t nwords = nbytes / 8;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     uint64_t *w = reinterpret_cast<uint64_t *>(dst);
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nwords; i += stride)
-        w[i] = splitmix64(base ^ i);
+        w[i] = splitmix64(base ^ (word0 + i));
     if (blockIdx.x == 0 && threadIdx.x < (nbytes & 7)) {
-        const uint64_t v = splitmix64(base ^ nwords);
+        const uint64_t v = splitmix64(base ^ (word0 + nwords));
         dst[nwords * 8 + threadIdx.x] = (uint8_t)(v >> (8 * threadIdx.x));
     }
 }
@@ -1104,14 +1105,14 @@ int rc_launch_read_probe(const uint8_t *d_src, uint64_t nbytes, uint32_t *d_out,
 }
 
 int rc_launch_fill(uint8_t *d_dst, uint64_t nbytes, uint64_t seed, uint64_t stream_id,
-                   void *stream) {
+                   uint64_t word0, void *stream) {
     if (nbytes == 0) return 0;
     const uint64_t base = (seed * 0x9E3779B97F4A7C15ull) ^ (stream_id << 34);
     uint64_t grid = (nbytes / 8 + 255) / 256;
     if (grid > 8192) grid = 8192;
     if (grid == 0) grid = 1;
     hipLaunchKernelGGL(rc_fill_kernel, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream,
-                       d_dst, nbytes, base);
+                       d_dst, nbytes, base, word0);
     return launch_status("rc_fill_kernel");
 }
 

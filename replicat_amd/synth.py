@@ -43,3 +43,37 @@ def seeded_key(seed: int) -> bytes:
     if int(w[0]) == 0:
         w[0] = np.uint64(1)
     return w.astype('<u8').tobytes()
+
+
+# ------------------------------------------------------------------ config 5: edited copies
+
+EDIT_KINDS = ('overwrite1', 'insert4', 'insert1')
+
+
+def edit_plan(n_streams: int = 1024, n_edit: int = 512, size: int = 64 << 20, seed: int = 5):
+    """``n_edit`` of the ``n_streams`` synthetic streams (a seeded
+    choice) get one edit each at a seeded offset, cycling through a 1-byte overwrite (XOR 0x5a),
+    a 4-byte insert and a 1-byte insert.  Returns ``[(stream, kind, offset, payload)]`` sorted
+    by stream; ``payload`` is the inserted bytes (empty for an overwrite)."""
+    import random
+    rnd = random.Random(seed)
+    ids = sorted(rnd.sample(range(n_streams), n_edit))
+    plan = []
+    for k, sid in enumerate(ids):
+        kind = EDIT_KINDS[k % 3]
+        if kind == 'overwrite1':
+            plan.append((sid, kind, rnd.randrange(size), b''))
+        else:
+            n = 4 if kind == 'insert4' else 1
+            plan.append((sid, kind, rnd.randrange(size + 1), rnd.randbytes(n)))
+    return plan
+
+
+def apply_edit(data: np.ndarray, kind: str, offset: int, payload: bytes) -> np.ndarray:
+    """The edited copy of a stream (a new array; ``data`` is left alone)."""
+    if kind == 'overwrite1':
+        out = data.copy()
+        out[offset] ^= 0x5A
+        return out
+    ins = np.frombuffer(payload, dtype=np.uint8)
+    return np.concatenate([data[:offset], ins, data[offset:]])

@@ -264,6 +264,97 @@ def make_digests(pool, quick=False):
     return out
 
 
+# ------------------------------------------------- large configs (3 ii, 5): large.json
+
+def _ref_ends(mn, mx, pieces, params=None):
+    ends, acc = [], 0
+    for n in ref_lengths(mn, mx, pieces, params):
+        acc += n
+        ends.append(acc)
+    return ends
+
+
+def make_config3ii(stream_id=0, size=64 << 30, tail=1 << 20, piece=16 << 20):
+    """Config 3 (ii): ONE 64 GiB stream under the reference's snapshot framing -- 16 MiB pieces
+    (repository.py:1413-1452) whose last piece is the final 1 MiB (P = L - 1 MiB).  The bytes
+    are generated piece by piece, so the reference adapter never needs the whole stream."""
+    base = synth.stream_base(synth.DEFAULT_SEED, stream_id)
+
+    def piece_bytes(off, n):
+        w0, w1 = off // 8, (off + n + 7) // 8
+        words = synth.splitmix_words(base, w0, w1 - w0)
+        return words.view('<u1')[off - 8 * w0:off - 8 * w0 + n].tobytes()
+
+    def pieces():
+        P = size - tail
+        off = 0
+        while off < P:
+            n = min(piece, P - off)
+            yield piece_bytes(off, n)
+            off += n
+        yield piece_bytes(P, tail)
+
+    ends = _ref_ends(MIN_DEF, MAX_DEF, pieces())
+    return {'name': 'config3ii', 'stream': stream_id, 'seed': synth.DEFAULT_SEED, 'size': size,
+            'last_piece': size - tail, 'min': MIN_DEF, 'max': MAX_DEF, 'params': None,
+            'chunks': len(ends), 'sha256': cutlist_digest([ends]), 'first_ends': ends[:64],
+            'last_ends': ends[-16:]}
+
+
+def _config5_job(job):
+    sid, edit, size = job
+    import hashlib as _h
+    data = synth.stream_bytes(size, synth.DEFAULT_SEED, sid)
+    if edit is not None:
+        data = synth.apply_edit(data, edit[0], edit[1], bytes.fromhex(edit[2]))
+    raw = data.tobytes()
+    ends = _ref_ends(MIN_DEF, MAX_DEF, [raw])
+    digests, start = [], 0
+    for e in ends:
+        digests.append(_h.blake2b(raw[start:e]).digest())
+        start = e
+    return sid, ends, digests
+
+
+def make_config5(pool, n_streams=1024, n_edit=512, size=64 << 20):
+    """Config 5: re-chunk of the edited copies of config 2 (synth.edit_plan) and the dedup
+    ratio = bytes of edited-set chunks whose content (BLAKE2b-512, as replicat digests chunks,
+    repository.py:1462) occurs among the original set's chunks / edited-set bytes."""
+    plan = synth.edit_plan(n_streams, n_edit, size)
+    orig = pool.map(_config5_job, [(i, None, size) for i in range(n_streams)], chunksize=4)
+    orig_ends = [e for _, e, _ in sorted(orig, key=lambda r: r[0])]
+    known = {d for _, _, ds in orig for d in ds}
+    jobs = [(sid, (kind, off, payload.hex()), size) for sid, kind, off, payload in plan]
+    edited = sorted(pool.map(_config5_job, jobs, chunksize=4), key=lambda r: r[0])
+    dup = total = 0
+    per_kind = {}
+    for (sid, kind, off, payload), (sid2, ends, digests) in zip(plan, edited):
+        assert sid == sid2
+        start = 0
+        d_bytes = 0
+        for e, dg in zip(ends, digests):
+            if dg in known:
+                d_bytes += e - start
+            start = e
+        dup += d_bytes
+        total += ends[-1]
+        k = per_kind.setdefault(kind, [0, 0])
+        k[0] += d_bytes
+        k[1] += ends[-1]
+    unedited = (n_streams - n_edit) * size
+    return {'name': 'config5', 'streams': n_streams, 'edited': n_edit, 'size': size,
+            'seed': synth.DEFAULT_SEED, 'plan_seed': 5, 'min': MIN_DEF, 'max': MAX_DEF,
+            'params': None,
+            'original_sha256': cutlist_digest(orig_ends),
+            'edited_sha256': cutlist_digest([e for _, e, _ in edited]),
+            'edited_chunks': sum(len(e) for _, e, _ in edited),
+            'edited_first_ends': [e for _, e, _ in edited[:6]],
+            'dup_bytes_edited': dup, 'total_bytes_edited': total,
+            'dup_bytes_by_kind': per_kind,
+            'dedup_ratio_edited': dup / total,
+            'dedup_ratio_set': (dup + unedited) / (total + unedited)}
+
+
 # ------------------------------------------------------------- module surface
 
 from golden_surface import SURFACE_CASES, surface_call  # noqa: E402
@@ -327,6 +418,17 @@ def make_snapshots():
 
 def main():
     quick = '--quick' in sys.argv
+    if '--large' in sys.argv:
+        with mp.get_context('fork').Pool(8) as pool:
+            r3 = pool.apply_async(make_config3ii)
+            c5 = make_config5(pool)
+            print('config5', c5['dedup_ratio_edited'], c5['original_sha256'], flush=True)
+            c3 = r3.get()
+            print('config3ii', c3['chunks'], c3['sha256'], flush=True)
+        with open(os.path.join(HERE, 'large.json'), 'w') as f:
+            json.dump([c3, c5], f, separators=(',', ':'))
+            f.write('\n')
+        return
     if '--snapshots-only' in sys.argv:
         with open(os.path.join(HERE, 'snapshots.json'), 'w') as f:
             json.dump(make_snapshots(), f, separators=(',', ':'))
