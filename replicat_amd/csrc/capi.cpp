@@ -322,7 +322,8 @@ int upload_and_launch(rc_chunker *ch, Workspace &ws, const Plan &plan, ChainPara
     if (int rc = ws.d_desc.ensure(plan.bytes)) return rc;
     if (int rc = ws.d_records.ensure((plan.n_tiles + 1) * sizeof(TileRecord))) return rc;
     if (int rc = ws.d_scratch.ensure(std::max<uint64_t>(plan.scratch_entries, 1) * 8)) return rc;
-    if (int rc = ws.d_seg_counts.ensure(std::max<uint64_t>(plan.n_segs, 1) * 8)) return rc;
+    // counts, merge points, slice offsets and slices of the parallel join (kernels.hip)
+    if (int rc = ws.d_seg_counts.ensure(std::max<uint64_t>(plan.n_segs, 1) * 32)) return rc;
     HIP_TRY(hipMemcpyAsync(ws.d_desc.p, ws.h_desc.p, plan.bytes, hipMemcpyHostToDevice, stream));
     const StreamDesc d = desc_view(ws.d_desc.p, plan.n);
     std::array<hipEvent_t, 3> ev{};

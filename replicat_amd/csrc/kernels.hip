@@ -838,8 +838,155 @@ __global__ __launch_bounds__(512) void rc_spec_kernel(const KeyTables *__restric
     }
 }
 
+// ---- parallel join of the speculative lists (multi-segment streams)
+//
+// Three small launches instead of one wave walking every segment of a stream in turn (one
+// dependent memory round trip per hop: milliseconds for the ~800 segments of a 64 GiB
+// stream):
+//   merge  one wave per boundary k: the first position p >= g_k of list k-1 that is g_k itself
+//          or an entry of list k -- where segment k-1's chain becomes segment k's;
+//   scan   one wave per stream: the true chain is list 0 up to its merge point, then list 1
+//          from there up to its own merge point, ...; slice lengths, prefix offsets, count;
+//   copy   one wave per segment: its slice to the stream's cut array.
+// Whenever that structure does not hold (no merge inside a list, a list that ends without the
+// chain ending, merge points out of order) the stream is marked kNeedJoin and the sequential
+// join below computes it exactly.
+constexpr uint64_t kNoMerge = ~0ull;
+constexpr int64_t kNeedJoin = -2;
+
+__global__ __launch_bounds__(256) void rc_merge_kernel(StreamDesc d, uint64_t n_streams,
+                                                       ChainParams prm, uint64_t n_segs,
+                                                       const uint64_t *__restrict__ scratch,
+                                                       const uint64_t *__restrict__ seg_counts,
+                                                       uint64_t *__restrict__ seg_merge) {
+    const uint32_t lane = lane_id();
+    const uint64_t q = (uint64_t)blockIdx.x * (blockDim.x >> 6) +
+                       __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (q >= n_segs) return;
+    const uint64_t s = find_index(d.seg_base, n_streams + 1, q);
+    const uint64_t sb = sload(d.seg_base + s), nseg = sload(d.seg_base + s + 1) - sb;
+    const uint64_t k = q - sb;
+    if (nseg <= 1 || k == 0) return;
+    const uint64_t *A = scratch + sload(d.scratch_base + s) + (k - 1) * prm.seg_cap;
+    const uint64_t *B = A + prm.seg_cap;
+    const uint64_t ca = seg_counts[q - 1], cb = seg_counts[q];
+    uint64_t result = kNoMerge;
+    if (ca != ~0ull && cb != ~0ull) {
+        const uint64_t na = ca & ~(1ull << 63), nb = cb & ~(1ull << 63);
+        const uint64_t g = k * prm.seg_bytes;
+        // list k-1's entries at or past g are its last few (the chain's extension)
+        const uint64_t a0 = na > 64 ? na - 64 : 0;
+        const uint64_t ai = a0 + lane;
+        const uint64_t av = ai < na ? A[ai] : 0;
+        const uint64_t bv = lane < nb ? B[lane] : ~0ull;
+        const uint64_t b_last = lane_u64(bv, 63);
+        uint64_t cm = __ballot(ai < na && av >= g);
+        const bool whole = a0 == 0 || !(cm & 1ull);  // every entry >= g is in this window
+        for (; whole && cm; cm &= cm - 1) {
+            const int l = __builtin_ctzll(cm);
+            const uint64_t p = lane_u64(av, l);
+            if (p == g) {
+                result = (a0 + l + 1) | (0ull << 32);
+                break;
+            }
+            const uint64_t hit = __ballot(bv == p);
+            if (hit) {
+                result = (a0 + l + 1) | ((uint64_t)(__builtin_ctzll(hit) + 1) << 32);
+                break;
+            }
+            if (nb > 64 && p > b_last) break;  // beyond the first 64 entries: let the walk do it
+        }
+    }
+    if (lane == 0) seg_merge[q] = result;
+}
+
+__global__ __launch_bounds__(256) void rc_scan_kernel(StreamDesc d, uint64_t n_streams,
+                                                      const uint64_t *__restrict__ seg_counts,
+                                                      const uint64_t *__restrict__ seg_merge,
+                                                      uint64_t *__restrict__ seg_off,
+                                                      uint64_t *__restrict__ seg_slice,
+                                                      int64_t *__restrict__ counts) {
+    const uint32_t lane = lane_id();
+    const uint64_t s = (uint64_t)blockIdx.x * (blockDim.x >> 6) +
+                       __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (s >= n_streams) return;
+    const uint64_t sb = sload(d.seg_base + s), nseg = sload(d.seg_base + s + 1) - sb;
+    if (nseg <= 1) return;
+    const uint64_t cap = sload(d.cut_cap + s);
+    uint64_t carry = 0;
+    bool fail = false, ended = false;
+    // every segment's slice is written (~0 past the chain's end): the copy kernel trusts it
+    for (uint64_t k0 = 0; k0 < nseg; k0 += 64) {
+        const uint64_t k = k0 + lane, q = sb + k;
+        const bool valid = k < nseg;
+        const uint64_t c = valid ? seg_counts[q] : 0;
+        const uint64_t m_in = valid && k > 0 ? seg_merge[q] : 0;
+        const uint64_t m_out = k + 1 < nseg ? seg_merge[q + 1] : kNoMerge;
+        const uint64_t n_k = c & ~(1ull << 63);
+        const bool term = (c >> 63) != 0 && c != ~0ull;
+        const uint64_t lo = m_in >> 32;
+        const bool ends = m_out == kNoMerge;
+        const uint64_t hi = ends ? n_k : (m_out & 0xffffffffu);
+        bool bad = valid && (c == ~0ull || m_in == kNoMerge || lo > hi || (ends && !term));
+        // the chain reaches segment k only if no earlier segment ended it
+        const uint64_t end_mask = ended ? 0 : __ballot(valid && ends && !bad);
+        const uint64_t first_end = end_mask ? __builtin_ctzll(end_mask) : 64;
+        const bool active = valid && !ended && lane <= first_end;
+        const uint64_t bad_mask = __ballot(active && bad);
+        if (bad_mask) {
+            fail = true;
+            break;
+        }
+        uint64_t len = active ? hi - lo : 0, x = len;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {  // inclusive prefix sum over the wave
+            const uint64_t y = __shfl_up(x, off);
+            if (lane >= (uint32_t)off) x += y;
+        }
+        if (active) {
+            seg_off[q] = carry + x - len;
+            seg_slice[q] = lo | (hi << 32);
+        } else if (valid) {
+            seg_slice[q] = ~0ull;
+        }
+        carry += lane_u64(x, 63);
+        if (end_mask) ended = true;
+    }
+    if (lane == 0) counts[s] = fail ? kNeedJoin : carry > cap ? -1 : (int64_t)carry;
+}
+
+__global__ __launch_bounds__(256) void rc_copy_kernel(StreamDesc d, uint64_t n_streams,
+                                                      ChainParams prm, uint64_t n_segs,
+                                                      const uint64_t *__restrict__ scratch,
+                                                      const uint64_t *__restrict__ seg_off,
+                                                      const uint64_t *__restrict__ seg_slice,
+                                                      uint64_t *__restrict__ cuts,
+                                                      const int64_t *__restrict__ counts) {
+    const uint32_t lane = lane_id();
+    const uint64_t q = (uint64_t)blockIdx.x * (blockDim.x >> 6) +
+                       __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (q >= n_segs) return;
+    const uint64_t s = find_index(d.seg_base, n_streams + 1, q);
+    const uint64_t sb = sload(d.seg_base + s), nseg = sload(d.seg_base + s + 1) - sb;
+    if (nseg <= 1 || counts[s] < 0) return;
+    const uint64_t sl = seg_slice[q];
+    if (sl == ~0ull) return;
+    const uint64_t lo = sl & 0xffffffffu, hi = sl >> 32;
+    const uint64_t *src = scratch + sload(d.scratch_base + s) + (q - sb) * prm.seg_cap;
+    uint64_t *dst = cuts + sload(d.cut_base + s) + seg_off[q];
+    for (uint64_t i = lo + lane; i < hi; i += 64) dst[i - lo] = src[i];
+}
+
+// RC_JOIN_WALK=1 (tests, diagnostics): every multi-segment stream takes the sequential walk.
+__global__ __launch_bounds__(256) void rc_mark_kernel(StreamDesc d, uint64_t n_streams,
+                                                      int64_t *__restrict__ counts) {
+    const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s < n_streams && sload(d.seg_base + s + 1) - sload(d.seg_base + s) > 1)
+        counts[s] = kNeedJoin;
+}
+
 // Join kernel: one wave per multi-segment stream, following the true chain across the
-// speculative lists (see above).
+// speculative lists (see above).  Only streams the scan marked kNeedJoin.
 __global__ __launch_bounds__(256) void rc_join_kernel(const KeyTables *__restrict__ tab,
                                                       StreamDesc d, uint64_t n_streams,
                                                       ChainParams prm,
@@ -848,16 +995,17 @@ __global__ __launch_bounds__(256) void rc_join_kernel(const KeyTables *__restric
                                                       int64_t *__restrict__ counts,
                                                       const uint64_t *__restrict__ scratch,
                                                       const uint64_t *__restrict__ seg_counts) {
+    const uint64_t s = (uint64_t)blockIdx.x * (blockDim.x >> 6) +
+                       __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const bool need = s < n_streams && counts[s] == kNeedJoin;
+    if (!__syncthreads_or(need)) return;  // the usual case: nothing to walk in this group
     stage_tile_tables(tab);
+    if (!need) return;
     const uint64_t *full = reinterpret_cast<const uint64_t *>(s_tile_lds + kFullOff / 4);
     const uint64_t *tl = full, *th = full + 1024;
     const uint32_t lane = lane_id();
     const uint32_t lb_a = (lane & 31) * 4, lb_b = lb_a | 0x10000u;
-    const uint64_t s = (uint64_t)blockIdx.x * (blockDim.x >> 6) +
-                       __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (s >= n_streams) return;
     const uint64_t sb = sload(d.seg_base + s), nseg = sload(d.seg_base + s + 1) - sb;
-    if (nseg <= 1) return;  // written directly by the spec kernel
     const ChainStream st = chain_stream(d, s);
     uint64_t *out = cuts + sload(d.cut_base + s);
     const uint64_t cap = sload(d.cut_cap + s);
@@ -1025,6 +1173,11 @@ int launch_status(const char *what) {
     return 1;
 }
 
+bool rc_join_walk_only() {  // read per launch: tests switch it within one process
+    const char *e = getenv("RC_JOIN_WALK");
+    return e && e[0] == '1';
+}
+
 int cu_count() {
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 256;
@@ -1086,7 +1239,29 @@ int rc_launch_chain(const KeyTables *d_tables, StreamDesc desc, uint64_t n_strea
                        d_scratch, d_seg_counts);
     if (launch_status("rc_spec_kernel")) return 1;
     if (!any_multi) return 0;
-    const uint64_t jgrid = (n_streams + kChainWaves - 1) / kChainWaves;
+    // d_seg_counts holds 4 arrays of n_segs: counts, merge points, slice offsets, slices
+    uint64_t *seg_merge = d_seg_counts + n_segs, *seg_off = seg_merge + n_segs;
+    uint64_t *seg_slice = seg_off + n_segs;
+    const uint64_t sgrid = (n_segs + 3) / 4, jgrid = (n_streams + kChainWaves - 1) / kChainWaves;
+    if (!rc_join_walk_only()) {
+        hipLaunchKernelGGL(rc_merge_kernel, dim3((unsigned)sgrid), dim3(256), 0, st, desc,
+                           n_streams, prm, n_segs, (const uint64_t *)d_scratch,
+                           (const uint64_t *)d_seg_counts, seg_merge);
+        if (launch_status("rc_merge_kernel")) return 1;
+        hipLaunchKernelGGL(rc_scan_kernel, dim3((unsigned)jgrid), dim3(kChainWaves * kWaveSize), 0,
+                           st, desc, n_streams, (const uint64_t *)d_seg_counts,
+                           (const uint64_t *)seg_merge, seg_off, seg_slice, d_counts);
+        if (launch_status("rc_scan_kernel")) return 1;
+        hipLaunchKernelGGL(rc_copy_kernel, dim3((unsigned)sgrid), dim3(256), 0, st, desc,
+                           n_streams, prm, n_segs, (const uint64_t *)d_scratch,
+                           (const uint64_t *)seg_off, (const uint64_t *)seg_slice, d_cuts,
+                           (const int64_t *)d_counts);
+        if (launch_status("rc_copy_kernel")) return 1;
+    } else {
+        hipLaunchKernelGGL(rc_mark_kernel, dim3((unsigned)jgrid), dim3(kChainWaves * kWaveSize), 0,
+                           st, desc, n_streams, d_counts);
+        if (launch_status("rc_mark_kernel")) return 1;
+    }
     hipLaunchKernelGGL(rc_join_kernel, dim3((unsigned)jgrid), dim3(kChainWaves * kWaveSize), 0, st,
                        d_tables, desc, n_streams, prm, d_records, d_cuts, d_counts,
                        (const uint64_t *)d_scratch, (const uint64_t *)d_seg_counts);

@@ -270,12 +270,15 @@ def test_tile_records_vs_oracle(kind):
         base += nt
 
 
+@pytest.mark.parametrize('walk', ['0', '1'])
 @pytest.mark.parametrize('seg_bytes,ext', [(1 << 16, 0), (1 << 16, 1), (1 << 16, 4),
                                            (12 * 4096, 2), (1 << 20, 3)])
-def test_segmented_chains_vs_oracle(monkeypatch, seg_bytes, ext):
+def test_segmented_chains_vs_oracle(monkeypatch, seg_bytes, ext, walk):
     """Segment-parallel speculative chains + join, with tiny segments and short extensions
-    (ext 0 forces the join kernel to compute most steps itself)."""
+    (ext 0 forces the join kernel to compute most steps itself); walk=1 sends every stream
+    through the sequential join instead of the parallel merge/scan/copy."""
     o = _oracle()
+    monkeypatch.setenv('RC_JOIN_WALK', walk)
     monkeypatch.setenv('RC_SEGMENT_BYTES', str(seg_bytes))
     monkeypatch.setenv('RC_SEGMENT_EXT', str(ext))
     rnd = random.Random(seg_bytes + ext)
