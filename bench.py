@@ -126,6 +126,30 @@ def cpu_baseline(n_streams, size, seed, procs):
                       f'{wall:.1f} s wall incl. data generation)'}, ends
 
 
+# ---------------------------------------------------------------- PMC traffic (profiles/)
+
+def pmc_traffic(args, n, size):
+    """HBM bytes per rc_tile_kernel launch from the committed rocprofv3 PMC summary of this same
+    command (scripts/gpu_profile.sh -> scripts/summarize_profile.py: separate --pmc passes,
+    FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM, WRITE_SIZE as is), or None when no summary
+    covers this workload.  bench.py cannot read counters itself (that needs rocprofv3)."""
+    if not (args.config == '2' and args.key == 'ff' and n == 1024 and size == 64 << 20):
+        return None, None
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, 'profiles', 'r*', 'pmc_summary.json')),
+                    reverse=True):
+        try:
+            with open(f) as fh:
+                d = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        t = d.get('rc_tile_kernel', {})
+        if d.get('workload') == 'config2' and 'hbm_read_bytes_corrected' in t:
+            return (t['hbm_read_bytes_corrected'] + t.get('hbm_write_bytes', 0.0),
+                    os.path.relpath(f, ROOT))
+    return None, None
+
+
 # ------------------------------------------------------------------- multi-GPU plumbing
 
 def shard_ids(config, rank, n):
@@ -408,6 +432,7 @@ def main():
                     % (args.config, n, size >> 20, min_len, max_len, args.key))
         if edit is not None:
             workload += ' (512 of the 1024 edited, re-chunk + dedup check)'
+    traffic, traffic_src = pmc_traffic(args, n, size)
     result = None
     if rank == 0:
         cpu = None
@@ -464,7 +489,9 @@ def main():
                        'streams_per_gpu': n, 'stream_bytes': size, 'parallelism': f'streams/{world} ranks'},
             'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
                          'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4),
-                         'traffic': None, 'kernel': 'rc_tile_kernel',
+                         'traffic': None if traffic is None else round(traffic),
+                         'traffic_source': traffic_src,
+                         'algorithmic_bytes': bytes_per_step, 'kernel': 'rc_tile_kernel',
                          'kernel_ms': round(a_avg, 3), 'chain_kernel_ms': round(b_avg, 3)},
             'cpu_baseline': cpu,
             'parity_sha256': parity,

@@ -154,8 +154,13 @@ __device__ __forceinline__ void take_best(uint64_t k, uint64_t j, uint64_t &bk, 
 // issues all of the lane's loads -- unconditionally, at indices clamped into the range, so
 // the compiler cannot serialise them behind divergent branches -- then evaluates, so a round
 // costs one memory latency.
-constexpr int kScanUnroll = 16;
+constexpr int kScanUnroll = 16;  // edge kernel: a whole tile per wave
+#ifndef RC_CHAIN_SCAN_UNROLL
+#define RC_CHAIN_SCAN_UNROLL 8
+#endif
+constexpr int kChainScanUnroll = RC_CHAIN_SCAN_UNROLL;  // chain steps' rare exact fallback
 
+template <int kScanUnroll>
 __device__ __forceinline__ void scan_ranges(const uint64_t *tl, const uint64_t *th,
                                             const uint8_t *base, uint64_t a0, uint64_t b0,
                                             uint64_t a1, uint64_t b1, uint64_t &bk,
@@ -188,7 +193,10 @@ __device__ __forceinline__ void scan_ranges(const uint64_t *tl, const uint64_t *
 }
 
 // Best record over tiles [t_lo, t_hi) of one stream, loads issued up front per round.
-constexpr int kRecUnroll = 8;
+#ifndef RC_REC_UNROLL
+#define RC_REC_UNROLL 8
+#endif
+constexpr int kRecUnroll = RC_REC_UNROLL;
 
 __device__ __forceinline__ void scan_records(const TileRecord *rec, uint64_t t_lo, uint64_t t_hi,
                                              uint64_t &bk, uint64_t &bj) {
@@ -477,7 +485,7 @@ __device__ __forceinline__ void exact_tile(const uint64_t *tl, const uint64_t *t
     const uint64_t j0 = (t - sload(d.tile_base + s)) * kTileKeys;
     const uint64_t jb = min(j0 + kTileKeys - 1, sload(d.jneed + s));
     uint64_t bk = 0, bj = ~0ull;
-    scan_ranges(tl, th, sload_ptr(d.ptr + s), max(j0, (uint64_t)1), jb, 1, 0, bk, bj);
+    scan_ranges<kScanUnroll>(tl, th, sload_ptr(d.ptr + s), max(j0, (uint64_t)1), jb, 1, 0, bk, bj);
     wave_best(bk, bj);
     if (lane_id() == 0) {
         rec[t].key = bk;
@@ -562,7 +570,10 @@ __device__ __forceinline__ ChainStream chain_stream(const StreamDesc &d, uint64_
 // before a lane's first key comes from the previous lane by DPP.  Per lane: running maxima of
 // (top16 << 16 | valid 0x8000 | order) for the first and the last occurrence; the order is the
 // lane-local key index (0-255 head, 256-511 tail; a range holds at most 8190 keys).
-constexpr int kEdgeIters = 8;  // 256-key iterations whose loads are issued together
+#ifndef RC_EDGE_ITERS
+#define RC_EDGE_ITERS 4
+#endif
+constexpr int kEdgeIters = RC_EDGE_ITERS;  // 256-key iterations whose loads are issued together
 
 // One edge range [a, b] of keys scanned at top-16 precision in batches of kEdgeIters 256-key
 // iterations: load() issues a batch's words, compute() folds them into the lane's running
@@ -719,7 +730,7 @@ __device__ int chain_step(const uint64_t *tl, const uint64_t *th, const TileReco
                 if (__any(cand && fl != ll)) {
                     // a candidate lane holds its top-16 maximum twice: exact scan of the edges
                     uint64_t ek = 0, ej = ~0ull;
-                    scan_ranges(tl, th, st.base, a0, b0, a1, b1, ek, ej);
+                    scan_ranges<kChainScanUnroll>(tl, th, st.base, a0, b0, a1, b1, ek, ej);
                     take_best(ek, ej, bk, bj);
                     wave_best(bk, bj);
                 } else {
@@ -775,7 +786,12 @@ __device__ __forceinline__ uint64_t find_index(const uint64_t *base_arr, uint64_
 // Spec kernel: one wave per segment.  A one-segment stream writes its final cuts directly;
 // segment i of a longer stream writes its list to the scratch and its count (bit 63 set if the
 // chain ended inside the list: tail rule or stop).
-__global__ __launch_bounds__(512) void rc_spec_kernel(const KeyTables *__restrict__ tab,
+#ifndef RC_SPEC_WAVES
+#define RC_SPEC_WAVES 12
+#endif
+constexpr int kSpecWaves = RC_SPEC_WAVES;  // walkers per CU when there are enough segments
+
+__global__ __launch_bounds__(kSpecWaves * 64) void rc_spec_kernel(const KeyTables *__restrict__ tab,
                                                       StreamDesc d, uint64_t n_streams,
                                                       ChainParams prm, uint64_t n_segs,
                                                       const TileRecord *__restrict__ rec,
@@ -1232,7 +1248,7 @@ int rc_launch_chain(const KeyTables *d_tables, StreamDesc desc, uint64_t n_strea
     if (n_streams == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
     // one 144 KiB-LDS workgroup per CU: 4 walkers each, 8 once there are walkers for it
-    const uint64_t wpg = n_segs >= 8 * (uint64_t)cu_count() ? 8 : kChainWaves;
+    const uint64_t wpg = n_segs >= kSpecWaves * (uint64_t)cu_count() ? kSpecWaves : kChainWaves;
     const uint64_t grid = (n_segs + wpg - 1) / wpg;
     hipLaunchKernelGGL(rc_spec_kernel, dim3((unsigned)grid), dim3(wpg * kWaveSize), 0, st,
                        d_tables, desc, n_streams, prm, n_segs, d_records, d_cuts, d_counts,

@@ -13,11 +13,14 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+WORKLOAD = 'config2'              # bench.py's default: 1024 x 64 MiB
+PROBE_BYTES = 1024 * (64 << 20)   # rc_read_probe over the same arena (whole 16 KiB tiles)
 
 
 def short(name):
     for k in ('rc_tile_kernel', 'rc_edge_kernel', 'rc_chain_kernel', 'rc_spec_kernel',
-              'rc_join_kernel', 'rc_fill_kernel'):
+              'rc_join_kernel', 'rc_fill_kernel', 'rc_read_probe_kernel', 'rc_merge_kernel',
+              'rc_scan_kernel', 'rc_copy_kernel', 'rc_mark_kernel'):
         if k in name:
             return k
     return name[:60]
@@ -44,12 +47,25 @@ def main():
         for (k, c), v in agg.items():
             out.setdefault(k, {})[c] = sum(v) / len(v)
     for k, d in out.items():
+        if not isinstance(d, dict):
+            continue
         if 'FETCH_SIZE' in d:
             d['hbm_read_bytes_corrected'] = 2 * d['FETCH_SIZE'] * 1024
         if 'WRITE_SIZE' in d:
             d['hbm_write_bytes'] = d['WRITE_SIZE'] * 1024
         if 'GRBM_GUI_ACTIVE' in d and d.get('avg_ns'):
             d['effective_clock_ghz'] = d['GRBM_GUI_ACTIVE'] / 8 / d['avg_ns']
+    # calibration on a known byte count in the same access pattern (MI355X_MICROARCH.md §HBM:
+    # 'calibrate on a known byte count in your own access pattern'): the read probe streams
+    # exactly PROBE_BYTES with the tile kernel's loads (bench.py --calibrate, config 2)
+    probe = out.get('rc_read_probe_kernel', {})
+    if probe.get('FETCH_SIZE'):
+        factor = PROBE_BYTES / (probe['FETCH_SIZE'] * 1024)
+        out['calibration'] = {'probe_bytes': PROBE_BYTES, 'bytes_per_fetch_byte': factor}
+        for k, d in out.items():
+            if isinstance(d, dict) and 'FETCH_SIZE' in d:
+                d['hbm_read_bytes_calibrated'] = d['FETCH_SIZE'] * 1024 * factor
+    out['workload'] = WORKLOAD
     with open(os.path.join(dst, 'pmc_summary.json'), 'w') as f:
         json.dump(out, f, indent=1, sort_keys=True)
     print(json.dumps(out.get('rc_tile_kernel', {}), indent=1))
