@@ -156,7 +156,7 @@ __device__ __forceinline__ void take_best(uint64_t k, uint64_t j, uint64_t &bk, 
 // costs one memory latency.
 constexpr int kScanUnroll = 16;  // edge kernel: a whole tile per wave
 #ifndef RC_CHAIN_SCAN_UNROLL
-#define RC_CHAIN_SCAN_UNROLL 8
+#define RC_CHAIN_SCAN_UNROLL 4
 #endif
 constexpr int kChainScanUnroll = RC_CHAIN_SCAN_UNROLL;  // chain steps' rare exact fallback
 
@@ -194,7 +194,7 @@ __device__ __forceinline__ void scan_ranges(const uint64_t *tl, const uint64_t *
 
 // Best record over tiles [t_lo, t_hi) of one stream, loads issued up front per round.
 #ifndef RC_REC_UNROLL
-#define RC_REC_UNROLL 8
+#define RC_REC_UNROLL 4
 #endif
 constexpr int kRecUnroll = RC_REC_UNROLL;
 
@@ -602,13 +602,21 @@ struct EdgeRange {
         carry = 0;
     }
     __device__ bool more() const { return live && it0 * 256 <= nk; }
+    // One 16-byte load per lane and iteration (1 KiB per wave instruction).  A lane's block is
+    // clamped to the aligned block holding the last existing word: past the stream's end the
+    // lane's keys are invalid anyway, and a 16-byte block that holds a stream byte cannot
+    // cross a page, so the read is safe even with no padding after the stream.
     __device__ void load(uint32_t (&w)[kEdgeIters][4]) const {
         const uint32_t lane = lane_id();
 #pragma unroll
-        for (int i = 0; i < kEdgeIters; ++i)
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                w[i][k] = ld_u32(p + 4 * min((it0 + i) * 256 + lane * 4 + k, wlast));
+        for (int i = 0; i < kEdgeIters; ++i) {
+            const uint32_t o = min((it0 + i) * 256 + lane * 4, wlast & ~3u);
+            const u32x4 v = *as_global_x4(p + 4 * o);
+            w[i][0] = v.x;
+            w[i][1] = v.y;
+            w[i][2] = v.z;
+            w[i][3] = v.w;
+        }
     }
     __device__ void compute(const uint32_t (&w)[kEdgeIters][4], uint32_t lb_a, uint32_t lb_b,
                             uint32_t &acc_first, uint32_t &acc_last) {
@@ -787,7 +795,7 @@ __device__ __forceinline__ uint64_t find_index(const uint64_t *base_arr, uint64_
 // segment i of a longer stream writes its list to the scratch and its count (bit 63 set if the
 // chain ended inside the list: tail rule or stop).
 #ifndef RC_SPEC_WAVES
-#define RC_SPEC_WAVES 12
+#define RC_SPEC_WAVES 16
 #endif
 constexpr int kSpecWaves = RC_SPEC_WAVES;  // walkers per CU when there are enough segments
 
@@ -1247,7 +1255,7 @@ int rc_launch_chain(const KeyTables *d_tables, StreamDesc desc, uint64_t n_strea
                     uint64_t *d_seg_counts, bool any_multi, void *stream) {
     if (n_streams == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
-    // one 144 KiB-LDS workgroup per CU: 4 walkers each, 8 once there are walkers for it
+    // one 144 KiB-LDS workgroup per CU: 4 walkers each, 16 (128 VGPRs) once there are enough
     const uint64_t wpg = n_segs >= kSpecWaves * (uint64_t)cu_count() ? kSpecWaves : kChainWaves;
     const uint64_t grid = (n_segs + wpg - 1) / wpg;
     hipLaunchKernelGGL(rc_spec_kernel, dim3((unsigned)grid), dim3(wpg * kWaveSize), 0, st,

@@ -11,9 +11,12 @@ import torch  # noqa: E402
 from replicat_amd import _lib, synth  # noqa: E402
 from replicat_amd.chunker import GpuChunker, fill_splitmix  # noqa: E402
 
+# usage: diag_stamps.py [n_streams] [stream_mib] [min] [max]   (default: config 2)
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
-size = 64 << 20
-ch = GpuChunker(128_000, 5_120_000, b'\xff' * 16)
+size = (int(sys.argv[2]) if len(sys.argv) > 2 else 64) << 20
+mn = int(sys.argv[3]) if len(sys.argv) > 3 else 128_000
+mx = int(sys.argv[4]) if len(sys.argv) > 4 else 5_120_000
+ch = GpuChunker(mn, mx, b'\xff' * 16)
 pool = torch.empty(n * size, dtype=torch.uint8, device='cuda')
 ptrs = [pool.data_ptr() + i * size for i in range(n)]
 hs = torch.cuda.current_stream().cuda_stream
