@@ -1,0 +1,72 @@
+/*
+ * replicat_digest.h -- C ABI of the MI355X (gfx950) BLAKE2b chunk digests.
+ *
+ * Replaces, for the snapshot path, the per-chunk `self.props.hash_digest(output_chunk)` of
+ * /root/reference/replicat/repository.py:1462, i.e. replicat's default hashing adapter
+ * `blake2b(length=64)` (replicat/utils/adapters.py:195-197,224-225; default name
+ * repository.py:217): hashlib.blake2b(data, digest_size=length).digest(), which is RFC 7693
+ * BLAKE2b, unkeyed, without salt or personalisation.  The keyed uses of that adapter (KDF, MAC:
+ * adapters.py:203-221, encrypted repositories only) are not provided.
+ *
+ * Digests live in 64-byte slots: the digest of message i (or of cut slot s) is the first
+ * digest_size bytes of slot i (s); the rest of the slot is zero.  Implemented by
+ * replicat_amd/csrc/{capi_digest.cpp,blake2b.hip} in replicat_amd/libreplicat_chunker.so.
+ */
+#ifndef REPLICAT_DIGEST_H
+#define REPLICAT_DIGEST_H
+
+#include <stdint.h>
+
+#include "replicat_chunker.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RC_DIGEST_SLOT 64
+#define RC_ERR_DIGEST_SIZE 4 /* "digest_size must be between 1 and 64 bytes": hashlib.blake2b's
+                                ValueError for the adapter's `length` (adapters.py:196-197) */
+
+typedef struct rc_hasher rc_hasher;
+
+/* `blake2b(length=digest_size)` (adapters.py:196-197) bound to HIP device `device`. */
+int rc_blake2b_create(uint32_t digest_size, int device, rc_hasher **out);
+void rc_blake2b_destroy(rc_hasher *h);
+uint32_t rc_blake2b_digest_size(const rc_hasher *h);
+
+/* `digest(data)` (adapters.py:224-225) of n DEVICE buffers d_ptrs[i] of lens[i] bytes (any
+ * alignment; NULL allowed for an empty buffer) into d_out + 64 * i.  Enqueued on hip_stream;
+ * returns without synchronising. */
+int rc_blake2b_device(rc_hasher *h, uint64_t n, const uint8_t *const *d_ptrs,
+                      const uint64_t *lens, uint8_t *d_out, void *hip_stream);
+
+/* The same for n HOST buffers into host out + 64 * i: copies in, hashes, copies back; blocking. */
+int rc_blake2b_host(rc_hasher *h, uint64_t n, const uint8_t *const *ptrs, const uint64_t *lens,
+                    uint8_t *out);
+
+/* `hash_digest` of every chunk that rc_chunk_device wrote for the same streams (repository.py
+ * :1455-1462): chunk k of stream i is [cuts[cut_base[i]+k-1], cuts[cut_base[i]+k]) (from 0
+ * for k = 0), where cut_base is the capacity prefix of rc_cut_capacity(layout, ...).  Its digest
+ * goes to d_digests + 64 * (cut_base[i] + k).  Counts are read on the device (no host sync).
+ * Enqueued on hip_stream. */
+int rc_blake2b_chunks(rc_hasher *h, const rc_chunker *layout, uint64_t n,
+                      const uint8_t *const *d_streams, const uint64_t *lens,
+                      const uint64_t *d_cuts, const int64_t *d_counts, uint8_t *d_digests,
+                      void *hip_stream);
+
+/* rc_chunk_host (replicat_chunker.h) plus the digest of every chunk, the snapshot loop's
+ * chunkify + hash_digest over host streams: digests[64 * (cut_base[i] + k)].  Blocking. */
+int rc_chunk_digest_host(rc_chunker *ch, rc_hasher *h, uint64_t n, const uint8_t *const *streams,
+                         const uint64_t *lens, const uint64_t *last_piece, uint32_t flags,
+                         uint64_t *cuts, int64_t *counts, uint8_t *digests);
+
+/* Kernel timing for bench.py: while enabled, each rc_blake2b_* enqueue records HIP events around
+ * its kernels on the launch stream; read returns the summed milliseconds and clears. */
+int rc_blake2b_timing_enable(rc_hasher *h, int enable);
+int rc_blake2b_timing_read(rc_hasher *h, double *ms, uint64_t *calls);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* REPLICAT_DIGEST_H */

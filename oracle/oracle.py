@@ -55,6 +55,10 @@ def lib():
                                           _p, _p, ctypes.c_int]
         L.oc_fill_splitmix.restype = None
         L.oc_fill_splitmix.argtypes = [_p, _u64, _u64, _u64]
+        L.oc_blake2b.restype = ctypes.c_int
+        L.oc_blake2b.argtypes = [_p, _u64, ctypes.c_uint32, _p]
+        L.oc_blake2b_chunks.restype = ctypes.c_int
+        L.oc_blake2b_chunks.argtypes = [_p, _p, _u64, ctypes.c_uint32, _p]
         _lib = L
     return _lib
 
@@ -150,3 +154,27 @@ def chunk_streams_mt(bufs, lens, pstarts, min_length, max_length, params=None, t
                               L.ctypes.data, P.ctypes.data, base.ctypes.data, cap.ctypes.data,
                               cuts.ctypes.data, counts.ctypes.data, threads)
     return [cuts[int(b):int(b) + int(c)].tolist() for b, c in zip(base, counts)]
+
+
+def blake2b(data, digest_size=64):
+    """oracle/blake2b_oracle.c: RFC 7693 BLAKE2b of `data` (what hashlib.blake2b(data,
+    digest_size=...).digest() returns; adapters.py:224-225)."""
+    arr = np.frombuffer(bytes(data), dtype=np.uint8)
+    out = np.zeros(64, dtype=np.uint8)
+    rc = lib().oc_blake2b(arr.ctypes.data if arr.size else None, arr.size, digest_size,
+                          out.ctypes.data)
+    if rc:
+        raise ValueError('digest_size must be between 1 and 64 bytes')
+    return out[:digest_size].tobytes()
+
+
+def blake2b_chunks(stream, ends, digest_size=64):
+    """Digest slots (n x 64 bytes) of the chunks [ends[k-1], ends[k]) of one host stream."""
+    arr = np.ascontiguousarray(np.frombuffer(stream, dtype=np.uint8)
+                               if not isinstance(stream, np.ndarray) else stream)
+    e = np.ascontiguousarray(np.asarray(ends, dtype=np.uint64))
+    out = np.zeros((len(e), 64), dtype=np.uint8)
+    if len(e):
+        assert lib().oc_blake2b_chunks(arr.ctypes.data, e.ctypes.data, len(e), digest_size,
+                                       out.ctypes.data) == 0
+    return out

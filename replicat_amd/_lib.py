@@ -16,14 +16,17 @@ RC_OK = 0
 RC_ERR_KEY_LENGTH = 1
 RC_ERR_MIN_GT_MAX = 2
 RC_ERR_BAD_KEY = 3
+RC_ERR_DIGEST_SIZE = 4
 RC_ERR_ARGUMENT = 10
 RC_ERR_ALIGN = 11
 RC_ERR_HIP = 12
 RC_ERR_OVERFLOW = 13
 RC_ERR_NO_DEVICE = 14
 RC_OPEN = 1
+RC_DIGEST_SLOT = 64
 
-# every symbol include/replicat_chunker.h declares: name -> (restype, argtypes)
+# every symbol include/replicat_chunker.h and include/replicat_digest.h declare:
+# name -> (restype, argtypes)
 _u64, _i64, _u32, _int, _p = ctypes.c_uint64, ctypes.c_int64, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p
 SIGNATURES = {
     'rc_version': (_int, []),
@@ -47,6 +50,16 @@ SIGNATURES = {
     'rc_tables_key': (_int, [_p, _u64, _p, _p, _p]),
     'rc_tile_records': (_int, [_p, _u64, _p, _p, _p, _p, _p, _u64, ctypes.POINTER(_u64)]),
     'rc_tile_keys': (_u64, []),
+    # replicat_digest.h
+    'rc_blake2b_create': (_int, [_u32, _int, ctypes.POINTER(_p)]),
+    'rc_blake2b_destroy': (None, [_p]),
+    'rc_blake2b_digest_size': (_u32, [_p]),
+    'rc_blake2b_device': (_int, [_p, _u64, _p, _p, _p, _p]),
+    'rc_blake2b_host': (_int, [_p, _u64, _p, _p, _p]),
+    'rc_blake2b_chunks': (_int, [_p, _p, _u64, _p, _p, _p, _p, _p, _p]),
+    'rc_chunk_digest_host': (_int, [_p, _p, _u64, _p, _p, _p, _u32, _p, _p, _p]),
+    'rc_blake2b_timing_enable': (_int, [_p, _int]),
+    'rc_blake2b_timing_read': (_int, [_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_u64)]),
 }
 
 
@@ -97,7 +110,7 @@ def check(code):
     if code == RC_OK:
         return
     msg = last_error()
-    if code in (RC_ERR_KEY_LENGTH, RC_ERR_MIN_GT_MAX, RC_ERR_BAD_KEY):
+    if code in (RC_ERR_KEY_LENGTH, RC_ERR_MIN_GT_MAX, RC_ERR_BAD_KEY, RC_ERR_DIGEST_SIZE):
         raise ValueError(msg)
     if code == RC_ERR_NO_DEVICE:
         raise ChunkerUnavailable(msg)

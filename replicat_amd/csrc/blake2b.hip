@@ -1,0 +1,357 @@
+// blake2b.hip -- BLAKE2b digests of chunks on gfx950.
+//
+// What it replaces: the per-chunk `self.props.hash_digest(output_chunk)` of replicat's snapshot
+// loop (/root/reference/replicat/repository.py:1462), i.e. `blake2b(length).digest(data)` =
+// `hashlib.blake2b(data, digest_size=length).digest()` (replicat/utils/adapters.py:195-225;
+// default length 64, repository.py:217).  hashlib's BLAKE2b is RFC 7693: unkeyed, no salt or
+// personalisation, parameter block word 0 = 0x01010000 ^ digest_size.
+//
+// Shape of the work.  BLAKE2b is a chain over 128-byte blocks: one chunk's compressions are
+// strictly sequential, so a chunk's latency is (#blocks) x (one compression's dependent
+// instruction stream).  The only parallelism inside a compression is the four G functions of a
+// column (or diagonal) step, so a QUAD of lanes hashes one chunk: lane q owns state column q
+// (v[q], v[4+q], v[8+q], v[12+q]) and chaining words h[q], h[q+4].  The diagonal step rotates
+// rows b/c/d by 1/2/3 lanes inside the quad with DPP quad_perm moves and back again -- 12 moves
+// per round, no LDS.  A compression is ~600 VALU per lane instead of ~1900 for one lane per
+// chunk, which is what bounds a 5 MB chunk (the critical path of config 2).
+//
+// The message schedule sigma makes lane q read word sigma[r][2q] (lane-dependent) in round r,
+// so the block is staged in LDS (two ds_write_b128 per lane: lane q writes bytes 32q..32q+31)
+// and each lane reads its four words per round through 40 precomputed LDS pointers.
+//
+// Loads: chunk starts are 4-aligned inside a stream except a stream's tail chunk, so every
+// lane loads 9 dwords from its 4-aligned base and funnels them with v_alignbyte (a no-op shift
+// when aligned).  Two blocks are kept in flight (one being hashed, the next two loaded).  The
+// final block clamps its dword addresses to the last dword holding chunk bytes and masks the
+// bytes past the chunk end: nothing beyond a chunk's last dword is ever read.
+//
+// Roofline: VALU issue, not HBM (64 GiB of chunks is ~1 TB/s of reads at the rates reached).
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "digest_kernels.h"
+
+namespace {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// chunk bytes are read through global-address-space pointers: flat loads would also count
+// against lgkmcnt and make every LDS message read wait for the blocks in flight
+#define GLOBAL __attribute__((address_space(1)))
+typedef const GLOBAL uint8_t *gbytes;
+
+constexpr uint64_t kIV[8] = {0x6a09e667f3bcc908ull, 0xbb67ae8584caa73bull, 0x3c6ef372fe94f82bull,
+                             0xa54ff53a5f1d36f1ull, 0x510e527fade682d1ull, 0x9b05688c2b3e6c1full,
+                             0x1f83d9abfb41bd6bull, 0x5be0cd19137e2179ull};
+
+constexpr uint8_t kSigma[10][16] = {
+    {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
+    {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3},
+    {11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4},
+    {7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8},
+    {9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13},
+    {2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9},
+    {12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11},
+    {13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10},
+    {6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5},
+    {10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0}};
+
+// word that lane q reads as message input k (0,1: column step; 2,3: diagonal step) in round r,
+// packed 4 bits per lane so that one v_bfe per (r, k) extracts it
+constexpr uint32_t sigma_pack(int r, int k) {
+    uint32_t p = 0;
+    for (int q = 0; q < 4; ++q) {
+        const int idx = k < 2 ? 2 * q + k : 8 + 2 * q + (k - 2);
+        p |= uint32_t(kSigma[r][idx]) << (4 * q);
+    }
+    return p;
+}
+
+// quad_perm controls: output lane j takes input lane perm[j]
+constexpr int kRot1 = 0x39;  // [1,2,3,0]
+constexpr int kRot2 = 0x4E;  // [2,3,0,1]
+constexpr int kRot3 = 0x93;  // [3,0,1,2]
+
+template <int C>
+__device__ __forceinline__ uint64_t quad_perm(uint64_t x) {
+    const uint32_t lo = __builtin_amdgcn_mov_dpp(static_cast<int>(x), C, 0xF, 0xF, true);
+    const uint32_t hi = __builtin_amdgcn_mov_dpp(static_cast<int>(x >> 32), C, 0xF, 0xF, true);
+    return (uint64_t(hi) << 32) | lo;
+}
+
+template <int N>
+__device__ __forceinline__ uint64_t rotr(uint64_t x) {
+    const uint32_t lo = static_cast<uint32_t>(x), hi = static_cast<uint32_t>(x >> 32);
+    uint32_t rl, rh;
+    if constexpr (N == 32) {
+        rl = hi;
+        rh = lo;
+    } else if constexpr (N < 32) {
+        rl = __builtin_amdgcn_alignbit(hi, lo, N);
+        rh = __builtin_amdgcn_alignbit(lo, hi, N);
+    } else {
+        rl = __builtin_amdgcn_alignbit(lo, hi, N - 32);
+        rh = __builtin_amdgcn_alignbit(hi, lo, N - 32);
+    }
+    return (uint64_t(rh) << 32) | rl;
+}
+
+__device__ __forceinline__ void g_mix(uint64_t &a, uint64_t &b, uint64_t &c, uint64_t &d,
+                                      uint64_t x, uint64_t y) {
+    a = a + b + x;
+    d = rotr<32>(d ^ a);
+    c = c + d;
+    b = rotr<24>(b ^ c);
+    a = a + b + y;
+    d = rotr<16>(d ^ a);
+    c = c + d;
+    b = rotr<63>(b ^ c);
+}
+
+struct LaneCtx {
+    const uint64_t *mp[10][4];  // this lane's message words, per round row and input
+    uint64_t iv_c, iv_d;        // IV[q], IV[q+4]
+    uint64_t t_mask, f_mask;    // ~0 on lane 0 (counter word v12) / lane 2 (final flag v14)
+};
+
+// One BLAKE2b compression of the quad's staged block; lane q updates h[q] (h0) and h[q+4] (h1).
+__device__ __forceinline__ void compress(uint64_t &h0, uint64_t &h1, const LaneCtx &cx, uint64_t t,
+                                         bool final) {
+    uint64_t a = h0, b = h1, c = cx.iv_c;
+    uint64_t d = cx.iv_d ^ (t & cx.t_mask) ^ (final ? cx.f_mask : 0ull);
+#pragma unroll
+    for (int r = 0; r < 12; ++r) {
+        const int s = r % 10;
+        const uint64_t m0 = *cx.mp[s][0], m1 = *cx.mp[s][1], m2 = *cx.mp[s][2], m3 = *cx.mp[s][3];
+        g_mix(a, b, c, d, m0, m1);  // column q
+        b = quad_perm<kRot1>(b);
+        c = quad_perm<kRot2>(c);
+        d = quad_perm<kRot3>(d);
+        g_mix(a, b, c, d, m2, m3);  // diagonal q
+        b = quad_perm<kRot3>(b);
+        c = quad_perm<kRot2>(c);
+        d = quad_perm<kRot1>(d);
+    }
+    h0 ^= a ^ c;
+    h1 ^= b ^ d;
+}
+
+struct Raw {
+    u32x4 x, y;
+    uint32_t z;
+};
+
+// 36 bytes from a 4-aligned address (the lane's 32 bytes plus the funnel spill)
+__device__ __forceinline__ Raw load_raw(gbytes a4) {
+    Raw r;
+    r.x = *reinterpret_cast<const GLOBAL u32x4 *>(a4);
+    r.y = *reinterpret_cast<const GLOBAL u32x4 *>(a4 + 16);
+    r.z = *reinterpret_cast<const GLOBAL uint32_t *>(a4 + 32);
+    return r;
+}
+
+__device__ __forceinline__ void stage(uint64_t *qb, int q, const Raw &w, uint32_t sh) {
+    const uint32_t sb = sh * 8;  // v_alignbyte takes the byte count; alignbit on bits is the same
+    u32x4 o0, o1;
+    o0.x = __builtin_amdgcn_alignbit(w.x.y, w.x.x, sb);
+    o0.y = __builtin_amdgcn_alignbit(w.x.z, w.x.y, sb);
+    o0.z = __builtin_amdgcn_alignbit(w.x.w, w.x.z, sb);
+    o0.w = __builtin_amdgcn_alignbit(w.y.x, w.x.w, sb);
+    o1.x = __builtin_amdgcn_alignbit(w.y.y, w.y.x, sb);
+    o1.y = __builtin_amdgcn_alignbit(w.y.z, w.y.y, sb);
+    o1.z = __builtin_amdgcn_alignbit(w.y.w, w.y.z, sb);
+    o1.w = __builtin_amdgcn_alignbit(w.z, w.y.w, sb);
+    *reinterpret_cast<u32x4 *>(qb + 4 * q) = o0;
+    *reinterpret_cast<u32x4 *>(qb + 4 * q + 2) = o1;
+}
+
+__device__ __forceinline__ uint32_t byte_mask(int64_t valid) {
+    return valid >= 4 ? 0xFFFFFFFFu : valid <= 0 ? 0u : (1u << (8 * valid)) - 1u;
+}
+
+}  // namespace
+
+// One quad per chunk; a workgroup is kB2Threads / 4 quads.  Items g = quad, quad + Q, ...
+__global__ __launch_bounds__(kB2Threads) void rc_b2_kernel(const B2Item *__restrict__ items,
+                                                           const uint64_t *__restrict__ d_total,
+                                                           uint64_t n_static, uint32_t outlen,
+                                                           uint8_t *__restrict__ out) {
+    __shared__ uint64_t blocks[kB2Threads / 4 * 16];
+    const int q = threadIdx.x & 3;
+    const int quad = threadIdx.x >> 2;
+    uint64_t *qb = blocks + quad * 16;
+
+    LaneCtx cx;
+#pragma unroll
+    for (int r = 0; r < 10; ++r)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) cx.mp[r][k] = qb + ((sigma_pack(r, k) >> (4 * q)) & 15u);
+    cx.iv_c = q == 0 ? kIV[0] : q == 1 ? kIV[1] : q == 2 ? kIV[2] : kIV[3];
+    cx.iv_d = q == 0 ? kIV[4] : q == 1 ? kIV[5] : q == 2 ? kIV[6] : kIV[7];
+    cx.t_mask = q == 0 ? ~0ull : 0ull;
+    cx.f_mask = q == 2 ? ~0ull : 0ull;
+    const uint64_t h0_init = (q == 0 ? kIV[0] ^ (0x01010000ull | outlen) : cx.iv_c);
+    const uint64_t h1_init = cx.iv_d;
+
+    const uint64_t total = d_total ? *d_total : n_static;
+    const uint64_t nq = uint64_t(gridDim.x) * (kB2Threads / 4);
+    for (uint64_t g = uint64_t(blockIdx.x) * (kB2Threads / 4) + quad; g < total; g += nq) {
+        const B2Item it = items[g];
+        gbytes p = reinterpret_cast<gbytes>(it.ptr);
+        const uint64_t len = it.len;
+        uint64_t h0 = h0_init, h1 = h1_init;
+        const uint64_t nfull = len ? (len - 1) / 128 : 0;  // non-final blocks
+
+        // lane base of block b: p + 128 b + 32 q, funnelled from its 4-aligned dword
+        gbytes lb = p + 32 * q;
+        const uint32_t sh = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(lb) & 3);
+        gbytes a4 = lb - sh;
+        // blocks b >= nfull are not loaded by the loop: clamp to block 0 (always readable when
+        // nfull > 0) so that every iteration issues the same loads
+        auto blk = [&](uint64_t b) { return a4 + 128 * (b < nfull ? b : 0); };
+        Raw A, B;
+        if (nfull) {
+            A = load_raw(blk(0));
+            B = load_raw(blk(1));
+        }
+        for (uint64_t b = 0; b < nfull; b += 2) {
+            stage(qb, q, A, sh);
+            A = load_raw(blk(b + 2));
+            compress(h0, h1, cx, (b + 1) * 128, false);
+            if (b + 1 < nfull) {
+                stage(qb, q, B, sh);
+                B = load_raw(blk(b + 3));
+                compress(h0, h1, cx, (b + 2) * 128, false);
+            }
+        }
+        // final block: rem = 1..128 bytes (0 only for an empty message)
+        {
+            const int64_t rem = static_cast<int64_t>(len - nfull * 128);
+            Raw F;
+            if (len) {
+                const uintptr_t last = (reinterpret_cast<uintptr_t>(p) + len - 1) & ~uintptr_t(3);
+                const uintptr_t f4 = reinterpret_cast<uintptr_t>(a4) + 128 * nfull;
+                uint32_t w[9];
+#pragma unroll
+                for (int i = 0; i < 9; ++i) {
+                    uintptr_t a = f4 + 4 * i;
+                    a = a < last ? a : last;
+                    w[i] = *reinterpret_cast<const GLOBAL uint32_t *>(a);
+                }
+                F.x = u32x4{w[0], w[1], w[2], w[3]};
+                F.y = u32x4{w[4], w[5], w[6], w[7]};
+                F.z = w[8];
+            } else {
+                F.x = F.y = u32x4{0u, 0u, 0u, 0u};
+                F.z = 0;
+            }
+            // funnel, then zero the bytes at or past the chunk end
+            const uint32_t sb = sh * 8;
+            const int64_t v0 = rem - 32 * q;
+            u32x4 o0, o1;
+            o0.x = __builtin_amdgcn_alignbit(F.x.y, F.x.x, sb) & byte_mask(v0);
+            o0.y = __builtin_amdgcn_alignbit(F.x.z, F.x.y, sb) & byte_mask(v0 - 4);
+            o0.z = __builtin_amdgcn_alignbit(F.x.w, F.x.z, sb) & byte_mask(v0 - 8);
+            o0.w = __builtin_amdgcn_alignbit(F.y.x, F.x.w, sb) & byte_mask(v0 - 12);
+            o1.x = __builtin_amdgcn_alignbit(F.y.y, F.y.x, sb) & byte_mask(v0 - 16);
+            o1.y = __builtin_amdgcn_alignbit(F.y.z, F.y.y, sb) & byte_mask(v0 - 20);
+            o1.z = __builtin_amdgcn_alignbit(F.y.w, F.y.z, sb) & byte_mask(v0 - 24);
+            o1.w = __builtin_amdgcn_alignbit(F.z, F.y.w, sb) & byte_mask(v0 - 28);
+            *reinterpret_cast<u32x4 *>(qb + 4 * q) = o0;
+            *reinterpret_cast<u32x4 *>(qb + 4 * q + 2) = o1;
+            compress(h0, h1, cx, len, true);
+        }
+        // digest bytes [8q, 8q+8) = h[q] and [32+8q, 40+8q) = h[q+4]; bytes >= outlen are zero
+        auto keep = [&](uint64_t h, int byte0) -> uint64_t {
+            const int v = static_cast<int>(outlen) - byte0;
+            return v >= 8 ? h : v <= 0 ? 0ull : h & ((1ull << (8 * v)) - 1);
+        };
+        uint64_t *o = reinterpret_cast<uint64_t *>(out + it.slot * kB2Slot);
+        o[q] = keep(h0, 8 * q);
+        o[4 + q] = keep(h1, 32 + 8 * q);
+    }
+}
+
+// Work list of the chunks rc_chunk_device wrote.  Pass 1 (one workgroup): exclusive prefix of
+// the per-stream chunk counts into chunk_off[0..n], total at chunk_off[n].
+__global__ __launch_bounds__(1024) void rc_b2_scan_kernel(const int64_t *__restrict__ counts,
+                                                          uint64_t n,
+                                                          uint64_t *__restrict__ chunk_off) {
+    __shared__ uint64_t part[1024];
+    const uint64_t per = (n + 1023) / 1024;
+    const uint64_t lo = threadIdx.x * per, hi = lo + per < n ? lo + per : n;
+    uint64_t s = 0;
+    for (uint64_t i = lo; i < hi; ++i) s += counts[i] > 0 ? uint64_t(counts[i]) : 0;
+    part[threadIdx.x] = s;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {  // inclusive Hillis-Steele scan
+        const uint64_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+        __syncthreads();
+        part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint64_t acc = part[threadIdx.x] - s;
+    for (uint64_t i = lo; i < hi; ++i) {
+        chunk_off[i] = acc;
+        acc += counts[i] > 0 ? uint64_t(counts[i]) : 0;
+    }
+    if (threadIdx.x == 1023) chunk_off[n] = part[1023];
+}
+
+// Pass 2: one workgroup per stream writes its chunks' items (start, length, cut slot).
+__global__ __launch_bounds__(256) void rc_b2_items_kernel(const uint64_t *__restrict__ ptrs,
+                                                          const uint64_t *__restrict__ cut_base,
+                                                          const uint64_t *__restrict__ cuts,
+                                                          const int64_t *__restrict__ counts,
+                                                          const uint64_t *__restrict__ chunk_off,
+                                                          B2Item *__restrict__ items) {
+    const uint64_t i = blockIdx.x;
+    const int64_t cnt = counts[i];
+    const uint64_t base = cut_base[i], o = chunk_off[i], p = ptrs[i];
+    for (int64_t k = threadIdx.x; k < cnt; k += blockDim.x) {
+        const uint64_t start = k ? cuts[base + k - 1] : 0, end = cuts[base + k];
+        items[o + k] = B2Item{p + start, end - start, base + k};
+    }
+}
+
+namespace {
+thread_local char g_b2_err[256];
+
+int b2_status(const char *what) {
+    const hipError_t e = hipGetLastError();
+    if (e == hipSuccess) return 0;
+    snprintf(g_b2_err, sizeof g_b2_err, "%s: %s", what, hipGetErrorString(e));
+    return 1;
+}
+
+unsigned b2_grid(uint64_t upper) {
+    const uint64_t quads = kB2Threads / 4;
+    uint64_t wg = (upper + quads - 1) / quads;
+    if (wg > kB2MaxGroups) wg = kB2MaxGroups;
+    return static_cast<unsigned>(wg ? wg : 1);
+}
+}  // namespace
+
+const char *rc_b2_launch_error(void) { return g_b2_err; }
+
+int rc_b2_launch_items(const B2Item *d_items, uint64_t n, uint32_t outlen, uint8_t *d_out,
+                       hipStream_t stream) {
+    if (!n) return 0;
+    rc_b2_kernel<<<b2_grid(n), kB2Threads, 0, stream>>>(d_items, nullptr, n, outlen, d_out);
+    return b2_status("rc_b2_kernel");
+}
+
+int rc_b2_launch_chunks(uint64_t n, const uint64_t *d_ptrs, const uint64_t *d_cut_base,
+                        const uint64_t *d_cuts, const int64_t *d_counts, uint64_t *d_chunk_off,
+                        B2Item *d_items, uint64_t items_cap, uint32_t outlen, uint8_t *d_out,
+                        hipStream_t stream) {
+    if (!n) return 0;
+    rc_b2_scan_kernel<<<1, 1024, 0, stream>>>(d_counts, n, d_chunk_off);
+    if (b2_status("rc_b2_scan_kernel")) return 1;
+    rc_b2_items_kernel<<<static_cast<unsigned>(n), 256, 0, stream>>>(d_ptrs, d_cut_base, d_cuts,
+                                                                    d_counts, d_chunk_off, d_items);
+    if (b2_status("rc_b2_items_kernel")) return 1;
+    rc_b2_kernel<<<b2_grid(items_cap), kB2Threads, 0, stream>>>(d_items, d_chunk_off + n, 0,
+                                                                outlen, d_out);
+    return b2_status("rc_b2_kernel");
+}

@@ -15,18 +15,26 @@
 #include <vector>
 
 #include "../../include/replicat_chunker.h"
+#include "capi_internal.h"
 #include "gclmul.h"
 
 using namespace rc;
+
+constexpr uint64_t kDigestSlot = RC_DIGEST_SLOT;
 
 namespace {
 
 thread_local char g_err[512];
 
+int vfail(int code, const char *fmt, va_list ap) {
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    return code;
+}
+
 int fail(int code, const char *fmt, ...) {
     va_list ap;
     va_start(ap, fmt);
-    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    vfail(code, fmt, ap);
     va_end(ap);
     return code;
 }
@@ -141,6 +149,14 @@ struct HostBuf {  // growable pinned host buffer
 
 }  // namespace
 
+int rc_fail(int code, const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vfail(code, fmt, ap);
+    va_end(ap);
+    return code;
+}
+
 struct rc_chunker {
     uint64_t min_length = 0, max_length = 0, window = 0;
     uint64_t seg_force = 0, ext_steps = 2;  // segment-parallel chains (see stage_descriptors)
@@ -167,7 +183,7 @@ struct rc_chunker {
     HostBuf h_out;
 
     // host-stream path scratch
-    DevBuf d_stage[2], d_hcuts[2], d_hcounts[2];
+    DevBuf d_stage[2], d_hcuts[2], d_hcounts[2], d_hdig[2];
     hipStream_t hstream[2] = {nullptr, nullptr};
 
     // timing
@@ -470,6 +486,7 @@ void rc_chunker_destroy(rc_chunker *ch) {
             ch->d_stage[i].release();
             ch->d_hcuts[i].release();
             ch->d_hcounts[i].release();
+            ch->d_hdig[i].release();
             if (ch->hstream[i]) (void)hipStreamDestroy(ch->hstream[i]);
         }
         ch->h_out.release();
@@ -585,11 +602,19 @@ int rc_chunk_device(rc_chunker *ch, uint64_t n, const uint8_t *const *d_streams,
                              static_cast<hipStream_t>(hip_stream));
 }
 
-int rc_chunk_host(rc_chunker *ch, uint64_t n, const uint8_t *const *streams, const uint64_t *lens,
-                  const uint64_t *last_piece, uint32_t flags, uint64_t *cuts, int64_t *counts) {
+}  // extern "C"
+
+namespace {
+
+// rc_chunk_host, and with a hasher rc_chunk_digest_host: batches of whole streams go through
+// pinned double-buffered copies; each batch's kernels (and digests) run on one of two streams.
+int chunk_host_impl(rc_chunker *ch, rc_hasher *hasher, uint64_t n, const uint8_t *const *streams,
+                    const uint64_t *lens, const uint64_t *last_piece, uint32_t flags,
+                    uint64_t *cuts, int64_t *counts, uint8_t *digests) {
     if (!ch) return fail(RC_ERR_ARGUMENT, "null chunker");
     if (n == 0) return RC_OK;
     if (!cuts || !counts) return fail(RC_ERR_ARGUMENT, "null output arrays");
+    if (hasher && !digests) return fail(RC_ERR_ARGUMENT, "null digest array");
     const bool open = (flags & RC_OPEN) != 0;
     if (int rc = validate_streams(n, streams, lens, open ? nullptr : last_piece, false)) return rc;
     std::lock_guard<std::mutex> lock(ch->mu);
@@ -653,6 +678,17 @@ int rc_chunk_host(rc_chunker *ch, uint64_t n, const uint8_t *const *streams, con
         int64_t *dn = static_cast<int64_t *>(ch->d_hcounts[slot].p);
         if (int rc = upload_and_launch(ch, ws, plan, chain_params(ch, plan, ~0ull, flags), dc, dn, st))
             return rc;
+        if (hasher) {
+            if (int rc = ch->d_hdig[slot].ensure(ncut * kDigestSlot)) return rc;
+            uint8_t *dd = static_cast<uint8_t *>(ch->d_hdig[slot].p);
+            std::vector<uint64_t> cb(nb);
+            for (uint64_t k = 0; k < nb; ++k) cb[k] = cut_base[i + k] - cut_base[i];
+            if (int rc = rc_hasher_enqueue_chunks(hasher, nb, dptr.data(), cb.data(), dc, dn, ncut,
+                                                  dd, st))
+                return rc;
+            HIP_TRY(hipMemcpyAsync(digests + cut_base[i] * kDigestSlot, dd, ncut * kDigestSlot,
+                                   hipMemcpyDeviceToHost, st));
+        }
         HIP_TRY(hipMemcpyAsync(cuts + cut_base[i], dc, ncut * 8, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipMemcpyAsync(counts + i, dn, nb * 8, hipMemcpyDeviceToHost, st));
         inflight[slot] = {i, nb};
@@ -663,6 +699,22 @@ int rc_chunk_host(rc_chunker *ch, uint64_t n, const uint8_t *const *streams, con
     if (int rc = finish(0)) return rc;
     if (int rc = finish(1)) return rc;
     return RC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rc_chunk_host(rc_chunker *ch, uint64_t n, const uint8_t *const *streams, const uint64_t *lens,
+                  const uint64_t *last_piece, uint32_t flags, uint64_t *cuts, int64_t *counts) {
+    return chunk_host_impl(ch, nullptr, n, streams, lens, last_piece, flags, cuts, counts, nullptr);
+}
+
+int rc_chunk_digest_host(rc_chunker *ch, rc_hasher *h, uint64_t n, const uint8_t *const *streams,
+                         const uint64_t *lens, const uint64_t *last_piece, uint32_t flags,
+                         uint64_t *cuts, int64_t *counts, uint8_t *digests) {
+    if (!h) return fail(RC_ERR_ARGUMENT, "null hasher");
+    return chunk_host_impl(ch, h, n, streams, lens, last_piece, flags, cuts, counts, digests);
 }
 
 uint64_t rc_tile_keys(void) { return kTileKeys; }

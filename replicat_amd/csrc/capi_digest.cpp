@@ -1,0 +1,328 @@
+// capi_digest.cpp -- host side of include/replicat_digest.h: BLAKE2b digests on the device.
+//
+// The hasher mirrors replicat's `blake2b(length)` hashing adapter (replicat/utils/adapters.py
+// :195-225): its digest_size, and `digest(data)` = hashlib.blake2b(data, digest_size).digest()
+// over many buffers per call.  Work lists are built here (buffers) or on the device (chunk
+// lists left in HBM by rc_chunk_device), then blake2b.hip hashes them one quad of lanes per
+// message.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <array>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "capi_internal.h"
+#include "digest_kernels.h"
+
+namespace {
+
+struct DevMem {
+    void *p = nullptr;
+    size_t n = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= n) return 0;
+        if (p) {
+            RC_HIP_TRY(hipDeviceSynchronize());
+            RC_HIP_TRY(hipFree(p));
+            p = nullptr;
+            n = 0;
+        }
+        const size_t want = (std::max<size_t>(bytes, 4096) + 4095) & ~size_t(4095);
+        RC_HIP_TRY(hipMalloc(&p, want));
+        n = want;
+        return 0;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
+struct PinnedMem {
+    void *p = nullptr;
+    size_t n = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= n) return 0;
+        if (p) RC_HIP_TRY(hipHostFree(p));
+        p = nullptr;
+        n = 0;
+        RC_HIP_TRY(hipHostMalloc(&p, std::max<size_t>(bytes, 4096), hipHostMallocDefault));
+        n = std::max<size_t>(bytes, 4096);
+        return 0;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
+struct Guard {
+    int prev = -1;
+    explicit Guard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~Guard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+}  // namespace
+
+struct rc_hasher {
+    uint32_t digest_size = 64;
+    int device = 0;
+    std::mutex mu;
+    struct Workspace {
+        PinnedMem h_stage;   // host-built descriptors / items
+        DevMem d_stage;      // their device copy
+        DevMem d_items;      // work list of the chunk path
+        hipEvent_t done = nullptr;
+        bool pending = false;
+    } ws[2];
+    unsigned next_ws = 0;
+    // blocking host path
+    DevMem d_data, d_out;
+    // timing
+    bool timing = false;
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<std::array<hipEvent_t, 2>> ev_rec;
+};
+
+namespace {
+
+using Workspace = rc_hasher::Workspace;
+
+int acquire(rc_hasher *h, Workspace *&out) {
+    Workspace &w = h->ws[h->next_ws++ & 1];
+    if (w.pending) {  // its previous call must have consumed the staging
+        RC_HIP_TRY(hipEventSynchronize(w.done));
+        w.pending = false;
+    }
+    out = &w;
+    return 0;
+}
+
+int timing_begin(rc_hasher *h, hipStream_t st, std::array<hipEvent_t, 2> &ev) {
+    if (!h->timing) return 0;
+    for (auto &e : ev) {
+        if (h->ev_pool.empty()) {
+            RC_HIP_TRY(hipEventCreate(&e));
+        } else {
+            e = h->ev_pool.back();
+            h->ev_pool.pop_back();
+        }
+    }
+    RC_HIP_TRY(hipEventRecord(ev[0], st));
+    return 0;
+}
+
+int timing_end(rc_hasher *h, hipStream_t st, std::array<hipEvent_t, 2> &ev) {
+    if (!h->timing) return 0;
+    RC_HIP_TRY(hipEventRecord(ev[1], st));
+    h->ev_rec.push_back(ev);
+    return 0;
+}
+
+int finish(rc_hasher *h, Workspace &w, hipStream_t st) {
+    RC_HIP_TRY(hipEventRecord(w.done, st));
+    w.pending = true;
+    (void)h;
+    return 0;
+}
+
+// digest of n device buffers: items built on the host
+int enqueue_items(rc_hasher *h, uint64_t n, const uint8_t *const *d_ptrs, const uint64_t *lens,
+                  uint8_t *d_out, hipStream_t st) {
+    Workspace *w = nullptr;
+    if (int rc = acquire(h, w)) return rc;
+    const size_t bytes = n * sizeof(B2Item);
+    if (int rc = w->h_stage.ensure(bytes)) return rc;
+    if (int rc = w->d_stage.ensure(bytes)) return rc;
+    B2Item *it = static_cast<B2Item *>(w->h_stage.p);
+    for (uint64_t i = 0; i < n; ++i) it[i] = B2Item{reinterpret_cast<uint64_t>(d_ptrs[i]), lens[i], i};
+    RC_HIP_TRY(hipMemcpyAsync(w->d_stage.p, w->h_stage.p, bytes, hipMemcpyHostToDevice, st));
+    std::array<hipEvent_t, 2> ev{};
+    if (int rc = timing_begin(h, st, ev)) return rc;
+    if (rc_b2_launch_items(static_cast<const B2Item *>(w->d_stage.p), n, h->digest_size, d_out, st))
+        return rc_fail(RC_ERR_HIP, "%s", rc_b2_launch_error());
+    if (int rc = timing_end(h, st, ev)) return rc;
+    return finish(h, *w, st);
+}
+
+int check_buffers(uint64_t n, const uint8_t *const *ptrs, const uint64_t *lens) {
+    if (n && (!ptrs || !lens)) return rc_fail(RC_ERR_ARGUMENT, "null buffer arrays");
+    for (uint64_t i = 0; i < n; ++i)
+        if (lens[i] && !ptrs[i])
+            return rc_fail(RC_ERR_ARGUMENT, "buffer %llu: null pointer", (unsigned long long)i);
+    return 0;
+}
+
+}  // namespace
+
+int rc_hasher_enqueue_chunks(rc_hasher *h, uint64_t n, const uint8_t *const *d_ptrs,
+                             const uint64_t *cut_base, const uint64_t *d_cuts,
+                             const int64_t *d_counts, uint64_t total_cap, uint8_t *d_out,
+                             hipStream_t st) {
+    if (!n) return 0;
+    std::lock_guard<std::mutex> lock(h->mu);
+    Guard g(h->device);
+    Workspace *w = nullptr;
+    if (int rc = acquire(h, w)) return rc;
+    // staging: ptr[n] cut_base[n] | device also: chunk_off[n+1]
+    const size_t up = 2 * n * sizeof(uint64_t);
+    if (int rc = w->h_stage.ensure(up)) return rc;
+    if (int rc = w->d_stage.ensure(up + (n + 1) * sizeof(uint64_t))) return rc;
+    if (int rc = w->d_items.ensure(std::max<uint64_t>(total_cap, 1) * sizeof(B2Item))) return rc;
+    uint64_t *u = static_cast<uint64_t *>(w->h_stage.p);
+    for (uint64_t i = 0; i < n; ++i) {
+        u[i] = reinterpret_cast<uint64_t>(d_ptrs[i]);
+        u[n + i] = cut_base[i];
+    }
+    RC_HIP_TRY(hipMemcpyAsync(w->d_stage.p, w->h_stage.p, up, hipMemcpyHostToDevice, st));
+    const uint64_t *d = static_cast<const uint64_t *>(w->d_stage.p);
+    uint64_t *chunk_off = static_cast<uint64_t *>(w->d_stage.p) + 2 * n;
+    std::array<hipEvent_t, 2> ev{};
+    if (int rc = timing_begin(h, st, ev)) return rc;
+    if (rc_b2_launch_chunks(n, d, d + n, d_cuts, d_counts, chunk_off,
+                            static_cast<B2Item *>(w->d_items.p), total_cap, h->digest_size, d_out,
+                            st))
+        return rc_fail(RC_ERR_HIP, "%s", rc_b2_launch_error());
+    if (int rc = timing_end(h, st, ev)) return rc;
+    return finish(h, *w, st);
+}
+
+extern "C" {
+
+int rc_blake2b_create(uint32_t digest_size, int device, rc_hasher **out) {
+    if (!out) return rc_fail(RC_ERR_ARGUMENT, "null output handle");
+    *out = nullptr;
+    if (digest_size < 1 || digest_size > 64)
+        return rc_fail(RC_ERR_DIGEST_SIZE, "digest_size must be between 1 and 64 bytes");
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count)
+        return rc_fail(RC_ERR_NO_DEVICE, "no HIP device %d", device);
+    Guard g(device);
+    rc_hasher *h = new rc_hasher;
+    h->digest_size = digest_size;
+    h->device = device;
+    for (auto &w : h->ws) {
+        const hipError_t e = hipEventCreateWithFlags(&w.done, hipEventDisableTiming);
+        if (e != hipSuccess) {
+            rc_blake2b_destroy(h);
+            return rc_fail(RC_ERR_HIP, "hipEventCreate failed: %s", hipGetErrorString(e));
+        }
+    }
+    *out = h;
+    return RC_OK;
+}
+
+void rc_blake2b_destroy(rc_hasher *h) {
+    if (!h) return;
+    {
+        Guard g(h->device);
+        (void)hipDeviceSynchronize();
+        for (auto &w : h->ws) {
+            w.h_stage.release();
+            w.d_stage.release();
+            w.d_items.release();
+            if (w.done) (void)hipEventDestroy(w.done);
+        }
+        h->d_data.release();
+        h->d_out.release();
+        for (auto &r : h->ev_rec)
+            for (auto e : r) (void)hipEventDestroy(e);
+        for (auto e : h->ev_pool) (void)hipEventDestroy(e);
+    }
+    delete h;
+}
+
+uint32_t rc_blake2b_digest_size(const rc_hasher *h) { return h ? h->digest_size : 0; }
+
+int rc_blake2b_device(rc_hasher *h, uint64_t n, const uint8_t *const *d_ptrs, const uint64_t *lens,
+                      uint8_t *d_out, void *hip_stream) {
+    if (!h) return rc_fail(RC_ERR_ARGUMENT, "null hasher");
+    if (n == 0) return RC_OK;
+    if (!d_out) return rc_fail(RC_ERR_ARGUMENT, "null output");
+    if (int rc = check_buffers(n, d_ptrs, lens)) return rc;
+    std::lock_guard<std::mutex> lock(h->mu);
+    Guard g(h->device);
+    return enqueue_items(h, n, d_ptrs, lens, d_out, static_cast<hipStream_t>(hip_stream));
+}
+
+int rc_blake2b_host(rc_hasher *h, uint64_t n, const uint8_t *const *ptrs, const uint64_t *lens,
+                    uint8_t *out) {
+    if (!h) return rc_fail(RC_ERR_ARGUMENT, "null hasher");
+    if (n == 0) return RC_OK;
+    if (!out) return rc_fail(RC_ERR_ARGUMENT, "null output");
+    if (int rc = check_buffers(n, ptrs, lens)) return rc;
+    std::lock_guard<std::mutex> lock(h->mu);
+    Guard g(h->device);
+    std::vector<uint64_t> off(n);
+    uint64_t total = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        off[i] = total;
+        total += (lens[i] + 15) & ~15ull;
+    }
+    if (int rc = h->d_data.ensure(total + 16)) return rc;
+    if (int rc = h->d_out.ensure(n * kB2Slot)) return rc;
+    std::vector<const uint8_t *> dp(n);
+    uint8_t *base = static_cast<uint8_t *>(h->d_data.p);
+    for (uint64_t i = 0; i < n; ++i) {
+        dp[i] = base + off[i];
+        if (lens[i]) RC_HIP_TRY(hipMemcpyAsync(base + off[i], ptrs[i], lens[i], hipMemcpyHostToDevice, nullptr));
+    }
+    if (int rc = enqueue_items(h, n, dp.data(), lens, static_cast<uint8_t *>(h->d_out.p), nullptr)) return rc;
+    RC_HIP_TRY(hipMemcpyAsync(out, h->d_out.p, n * kB2Slot, hipMemcpyDeviceToHost, nullptr));
+    RC_HIP_TRY(hipStreamSynchronize(nullptr));
+    return RC_OK;
+}
+
+int rc_blake2b_chunks(rc_hasher *h, const rc_chunker *layout, uint64_t n,
+                      const uint8_t *const *d_streams, const uint64_t *lens, const uint64_t *d_cuts,
+                      const int64_t *d_counts, uint8_t *d_digests, void *hip_stream) {
+    if (!h || !layout) return rc_fail(RC_ERR_ARGUMENT, "null hasher or chunker");
+    if (n == 0) return RC_OK;
+    if (!d_cuts || !d_counts || !d_digests) return rc_fail(RC_ERR_ARGUMENT, "null device arrays");
+    if (int rc = check_buffers(n, d_streams, lens)) return rc;
+    std::vector<uint64_t> caps(n), base(n);
+    const uint64_t total = rc_cut_capacity(layout, n, lens, caps.data());
+    uint64_t acc = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        base[i] = acc;
+        acc += caps[i];
+    }
+    return rc_hasher_enqueue_chunks(h, n, d_streams, base.data(), d_cuts, d_counts, total, d_digests,
+                                    static_cast<hipStream_t>(hip_stream));
+}
+
+int rc_blake2b_timing_enable(rc_hasher *h, int enable) {
+    if (!h) return rc_fail(RC_ERR_ARGUMENT, "null hasher");
+    h->timing = enable != 0;
+    return RC_OK;
+}
+
+int rc_blake2b_timing_read(rc_hasher *h, double *ms, uint64_t *calls) {
+    if (!h) return rc_fail(RC_ERR_ARGUMENT, "null hasher");
+    std::lock_guard<std::mutex> lock(h->mu);
+    Guard g(h->device);
+    double a = 0;
+    for (auto &r : h->ev_rec) {
+        RC_HIP_TRY(hipEventSynchronize(r[1]));
+        float x = 0;
+        RC_HIP_TRY(hipEventElapsedTime(&x, r[0], r[1]));
+        a += x;
+        for (auto e : r) h->ev_pool.push_back(e);
+    }
+    if (ms) *ms = a;
+    if (calls) *calls = h->ev_rec.size();
+    h->ev_rec.clear();
+    return RC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,24 @@
+// capi_internal.h -- what capi.cpp (chunker) and capi_digest.cpp (BLAKE2b) share.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/replicat_digest.h"
+
+// Sets the calling thread's rc_last_error() message and returns `code`.
+int rc_fail(int code, const char *fmt, ...);
+
+#define RC_HIP_TRY(expr)                                                                 \
+    do {                                                                                 \
+        const hipError_t e_ = (expr);                                                    \
+        if (e_ != hipSuccess)                                                            \
+            return rc_fail(RC_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(e_));   \
+    } while (0)
+
+// Enqueue on `st` the digests of the chunks of n device streams (d_ptrs: HOST array of device
+// pointers) whose cut lists sit at d_cuts[cut_base[i] ..] with d_counts[i] entries, into
+// d_out + 64 * (cut_base[i] + k).  total_cap = sum of the cut capacities (>= the chunk count).
+int rc_hasher_enqueue_chunks(rc_hasher *h, uint64_t n, const uint8_t *const *d_ptrs,
+                             const uint64_t *cut_base, const uint64_t *d_cuts,
+                             const int64_t *d_counts, uint64_t total_cap, uint8_t *d_out,
+                             hipStream_t st);

@@ -1,0 +1,27 @@
+// digest_kernels.h -- internal interface between blake2b.hip (kernels) and capi_digest.cpp.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+// One message to hash: device address, length in bytes, output slot (digest at out + 64 * slot).
+struct B2Item {
+    uint64_t ptr, len, slot;
+};
+
+constexpr int kB2Threads = 256;       // 4 waves, 64 quads per workgroup
+constexpr uint64_t kB2MaxGroups = 512;  // 2 waves per SIMD on 256 CUs; items beyond loop
+constexpr uint64_t kB2Slot = 64;      // bytes per digest slot (BLAKE2b's largest digest)
+
+const char *rc_b2_launch_error(void);
+
+// Digests of n items (host-built work list, already on the device).
+int rc_b2_launch_items(const B2Item *d_items, uint64_t n, uint32_t outlen, uint8_t *d_out,
+                       hipStream_t stream);
+
+// Digests of the chunks of n streams as rc_chunk_device wrote them: d_cuts at d_cut_base[i],
+// d_counts[i] chunks.  d_chunk_off has n + 1 entries; d_items holds items_cap (>= sum of
+// counts) entries.
+int rc_b2_launch_chunks(uint64_t n, const uint64_t *d_ptrs, const uint64_t *d_cut_base,
+                        const uint64_t *d_cuts, const int64_t *d_counts, uint64_t *d_chunk_off,
+                        B2Item *d_items, uint64_t items_cap, uint32_t outlen, uint8_t *d_out,
+                        hipStream_t stream);

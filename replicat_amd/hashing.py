@@ -1,0 +1,126 @@
+"""BLAKE2b chunk digests on the device.
+
+replicat's snapshot loop takes ``self.props.hash_digest(output_chunk)`` of every chunk it cuts
+(/root/reference/replicat/repository.py:1462).  The default hashing adapter is
+``blake2b(length=64)`` (repository.py:217; replicat/utils/adapters.py:195-197), whose
+``digest(data)`` is ``hashlib.blake2b(data, digest_size=length).digest()`` (adapters.py:224-225).
+
+``GpuBlake2b`` mirrors that adapter's unkeyed surface -- ``digest_size`` and ``digest(data)`` --
+and adds the batch entry points of include/replicat_digest.h:
+
+* ``digest_many(buffers)``          -- host buffers in, digests out (blocking);
+* ``digest_device(ptrs, lens, out)`` -- device buffers, digests left in HBM (64-byte slots);
+* ``digest_chunks(chunker, ...)``    -- the chunks a ``GpuChunker.chunk_device`` call left in
+  HBM, digested without a host round trip (digest of cut slot s at out + 64 s).
+
+The keyed uses of the adapter (KDF, MAC: adapters.py:203-221, encrypted repositories) are not
+provided.  There is no CPU fallback: without the HIP library every call raises.
+"""
+import ctypes
+
+import numpy as np
+
+from ._lib import RC_DIGEST_SLOT, check, lib
+from .chunker import _current_device, _ptr_array
+
+SLOT = RC_DIGEST_SLOT
+
+
+class GpuBlake2b:
+    """``blake2b(length=...)`` (adapters.py:195-197) on one HIP device."""
+
+    def __init__(self, *, length: int = 64, device=None):
+        if device is None:
+            device = _current_device()
+        if not isinstance(length, int):
+            raise TypeError(f'{type(length).__name__!r} object cannot be interpreted as an integer')
+        handle = ctypes.c_void_p()
+        check(lib().rc_blake2b_create(length if 0 <= length < 1 << 32 else 0, int(device),
+                                      ctypes.byref(handle)))
+        self._h = handle
+        self.digest_size = int(length)
+        self.device = int(device)
+
+    def close(self):
+        h, self._h = getattr(self, '_h', None), None
+        if h:
+            lib().rc_blake2b_destroy(h)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ host buffers
+
+    def digest(self, data) -> bytes:
+        """adapters.py:224-225 for one host buffer."""
+        return self.digest_many([data])[0]
+
+    def digest_many(self, buffers):
+        arrs = [np.frombuffer(b, dtype=np.uint8) if not isinstance(b, np.ndarray) else
+                np.ascontiguousarray(b).view(np.uint8).reshape(-1) for b in buffers]
+        n = len(arrs)
+        if n == 0:
+            return []
+        lens = _ptr_array([a.size for a in arrs])
+        ptrs = _ptr_array([a.ctypes.data if a.size else 0 for a in arrs])
+        out = np.zeros((n, SLOT), dtype=np.uint8)
+        check(lib().rc_blake2b_host(self._h, n, ptrs.ctypes.data, lens.ctypes.data,
+                                    out.ctypes.data))
+        return [out[i, :self.digest_size].tobytes() for i in range(n)]
+
+    # ---------------------------------------------------------------- device buffers
+
+    def digest_device(self, ptrs, lens, out_ptr, stream=0):
+        """Enqueue the digests of device buffers (raw pointers) into 64-byte slots at out_ptr."""
+        ptrs, lens = _ptr_array(ptrs), _ptr_array(lens)
+        check(lib().rc_blake2b_device(self._h, len(lens), ptrs.ctypes.data, lens.ctypes.data,
+                                      out_ptr, stream or None))
+
+    def digest_chunks(self, chunker, ptrs, lens, cuts_ptr, counts_ptr, out_ptr, stream=0):
+        """Enqueue the digests of the chunks ``chunker.chunk_device`` wrote for these streams:
+        the slot of cut s (``cuts_ptr`` layout, ``chunker.capacity(lens)``) is out + 64 s."""
+        ptrs, lens = _ptr_array(ptrs), _ptr_array(lens)
+        check(lib().rc_blake2b_chunks(self._h, chunker._h, len(lens), ptrs.ctypes.data,
+                                      lens.ctypes.data, cuts_ptr, counts_ptr, out_ptr,
+                                      stream or None))
+
+    # ---------------------------------------------------------------------- profiling
+
+    def timing(self, enable: bool):
+        check(lib().rc_blake2b_timing_enable(self._h, 1 if enable else 0))
+
+    def read_timing(self):
+        ms, n = ctypes.c_double(), ctypes.c_uint64()
+        check(lib().rc_blake2b_timing_read(self._h, ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
+
+
+def chunk_digest_host(chunker, hasher, buffers, last_piece=None, open_=False):
+    """The snapshot loop's chunkify + hash_digest over host streams in one device pass
+    (rc_chunk_digest_host): returns (cut-END arrays, per-stream (count x digest_size) digests)."""
+    from ._lib import RC_OPEN
+    arrs = [np.frombuffer(b, dtype=np.uint8) if not isinstance(b, np.ndarray) else b
+            for b in buffers]
+    n = len(arrs)
+    if n == 0:
+        return [], []
+    lens = _ptr_array([a.size for a in arrs])
+    ptrs = _ptr_array([a.ctypes.data if a.size else 0 for a in arrs])
+    last = _ptr_array(last_piece if last_piece is not None else np.zeros(n))
+    total, caps = chunker.capacity(lens)
+    cuts = np.zeros(max(total, 1), dtype=np.uint64)
+    counts = np.zeros(n, dtype=np.int64)
+    digests = np.zeros((max(total, 1), SLOT), dtype=np.uint8)
+    check(lib().rc_chunk_digest_host(chunker._h, hasher._h, n, ptrs.ctypes.data,
+                                     lens.ctypes.data, last.ctypes.data,
+                                     RC_OPEN if open_ else 0, cuts.ctypes.data,
+                                     counts.ctypes.data, digests.ctypes.data))
+    base = np.concatenate([[0], np.cumsum(caps)[:-1]]).astype(np.int64)
+    return ([cuts[b:b + c] for b, c in zip(base, counts)],
+            [digests[b:b + c, :hasher.digest_size] for b, c in zip(base, counts)])
+
+
+__all__ = ['GpuBlake2b', 'chunk_digest_host', 'SLOT']

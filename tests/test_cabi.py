@@ -13,13 +13,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def header_symbols():
-    text = open(os.path.join(ROOT, 'include', 'replicat_chunker.h')).read()
+    text = ''.join(open(os.path.join(ROOT, 'include', h)).read()
+                   for h in ('replicat_chunker.h', 'replicat_digest.h'))
     return sorted(set(re.findall(r'^\w[\w\s\*]*?\b(rc_\w+)\s*\(', text, re.M)))
 
 
 def test_exports_every_declared_symbol():
     syms = header_symbols()
     assert len(syms) >= 15
+    assert 'rc_blake2b_chunks' in syms and 'rc_chunk_digest_host' in syms
     lib = _lib.lib()
     for s in syms:
         assert hasattr(lib, s), s
