@@ -117,12 +117,19 @@ struct LaneCtx {
 // One BLAKE2b compression of the quad's staged block; lane q updates h[q] (h0) and h[q+4] (h1).
 __device__ __forceinline__ void compress(uint64_t &h0, uint64_t &h1, const LaneCtx &cx, uint64_t t,
                                          bool final) {
+    // all 40 message words of the lane up front: one LDS latency per block, not one per round
+    uint64_t m[10][4];
+#pragma unroll
+    for (int s = 0; s < 10; ++s)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) m[s][k] = *cx.mp[s][k];
+    __builtin_amdgcn_sched_barrier(0);
     uint64_t a = h0, b = h1, c = cx.iv_c;
     uint64_t d = cx.iv_d ^ (t & cx.t_mask) ^ (final ? cx.f_mask : 0ull);
 #pragma unroll
     for (int r = 0; r < 12; ++r) {
         const int s = r % 10;
-        const uint64_t m0 = *cx.mp[s][0], m1 = *cx.mp[s][1], m2 = *cx.mp[s][2], m3 = *cx.mp[s][3];
+        const uint64_t m0 = m[s][0], m1 = m[s][1], m2 = m[s][2], m3 = m[s][3];
         g_mix(a, b, c, d, m0, m1);  // column q
         b = quad_perm<kRot1>(b);
         c = quad_perm<kRot2>(c);
@@ -193,9 +200,26 @@ __global__ __launch_bounds__(kB2Threads) void rc_b2_kernel(const B2Item *__restr
     const uint64_t h0_init = (q == 0 ? kIV[0] ^ (0x01010000ull | outlen) : cx.iv_c);
     const uint64_t h1_init = cx.iv_d;
 
+    // One wave per SIMD (256 groups) unless items are plentiful: a BLAKE2b compression is
+    // VALU-issue bound, so a second wave on a SIMD halves the speed of the first -- and the
+    // longest chunk's wave sets the end of the launch.  Every group computes the same count.
     const uint64_t total = d_total ? *d_total : n_static;
-    const uint64_t nq = uint64_t(gridDim.x) * (kB2Threads / 4);
-    for (uint64_t g = uint64_t(blockIdx.x) * (kB2Threads / 4) + quad; g < total; g += nq) {
+    const uint64_t per_group = kB2Threads / 4;
+    uint64_t groups = total >= kB2TwoWaveItems ? kB2MaxGroups : kB2OneWaveGroups;
+    groups = groups < gridDim.x ? groups : gridDim.x;
+    const uint64_t need = (total + per_group - 1) / per_group;
+    groups = need < groups ? (need ? need : 1) : groups;
+    if (blockIdx.x >= groups) return;
+    const uint64_t nq = groups * per_group;
+    // Snake deal over the longest-first list: round r takes items [r nq, (r+1) nq), in quad order
+    // on even rounds and reversed on odd ones, so the quad that got the longest item of one
+    // round gets the shortest of the next (a wave's 16 quads stay on 16 neighbouring items).
+    const uint64_t gq = uint64_t(blockIdx.x) * per_group + quad;
+    for (uint64_t r0 = 0; r0 < total; r0 += 2 * nq)
+#pragma unroll 1
+    for (int odd = 0; odd < 2; ++odd) {
+        const uint64_t g = r0 + odd * nq + (odd ? nq - 1 - gq : gq);
+        if (g >= total) continue;
         const B2Item it = items[g];
         gbytes p = reinterpret_cast<gbytes>(it.ptr);
         const uint64_t len = it.len;
@@ -214,15 +238,20 @@ __global__ __launch_bounds__(kB2Threads) void rc_b2_kernel(const B2Item *__restr
             A = load_raw(blk(0));
             B = load_raw(blk(1));
         }
-        for (uint64_t b = 0; b < nfull; b += 2) {
+        // two blocks per iteration with fixed register roles: copying A = B would make the
+        // compiler wait for B's loads (vmcnt(0)) and collapse the prefetch distance
+        uint64_t b = 0;
+        for (; b + 2 <= nfull; b += 2) {
             stage(qb, q, A, sh);
             A = load_raw(blk(b + 2));
             compress(h0, h1, cx, (b + 1) * 128, false);
-            if (b + 1 < nfull) {
-                stage(qb, q, B, sh);
-                B = load_raw(blk(b + 3));
-                compress(h0, h1, cx, (b + 2) * 128, false);
-            }
+            stage(qb, q, B, sh);
+            B = load_raw(blk(b + 3));
+            compress(h0, h1, cx, (b + 2) * 128, false);
+        }
+        if (b < nfull) {  // odd count: A holds block b
+            stage(qb, q, A, sh);
+            compress(h0, h1, cx, (b + 1) * 128, false);
         }
         // final block: rem = 1..128 bytes (0 only for an empty message)
         {
@@ -272,8 +301,23 @@ __global__ __launch_bounds__(kB2Threads) void rc_b2_kernel(const B2Item *__restr
     }
 }
 
-// Work list of the chunks rc_chunk_device wrote.  Pass 1 (one workgroup): exclusive prefix of
-// the per-stream chunk counts into chunk_off[0..n], total at chunk_off[n].
+// Work list of the chunks rc_chunk_device wrote, longest first.
+//
+// The digest kernel hands items out round-robin in list order (quad g of the grid takes items
+// g, g + Q, ..): with the list sorted by decreasing length, the 16 quads of a wave get items of
+// about the same length (a wave runs as long as its longest item) and the grid gets the longest
+// items first (LPT), so no wave is left holding a 5 MB chunk at the end.  The order is a bucket
+// sort on (floor(log2(len+1)), next two bits): 256 buckets, exact enough for scheduling.
+
+__device__ __forceinline__ uint32_t len_bucket(uint64_t len) {
+    const uint64_t x = len + 1;
+    const int e = 63 - __clzll(static_cast<long long>(x));
+    const uint32_t m = e >= 2 ? static_cast<uint32_t>(x >> (e - 2)) & 3u : (e == 1 ? (x & 1u) << 1 : 0u);
+    return 255u - (4u * static_cast<uint32_t>(e) + m);  // 0 = longest
+}
+
+// Pass 1 (one workgroup): exclusive prefix of the per-stream chunk counts into chunk_off[0..n],
+// total at chunk_off[n].
 __global__ __launch_bounds__(1024) void rc_b2_scan_kernel(const int64_t *__restrict__ counts,
                                                           uint64_t n,
                                                           uint64_t *__restrict__ chunk_off) {
@@ -298,19 +342,69 @@ __global__ __launch_bounds__(1024) void rc_b2_scan_kernel(const int64_t *__restr
     if (threadIdx.x == 1023) chunk_off[n] = part[1023];
 }
 
-// Pass 2: one workgroup per stream writes its chunks' items (start, length, cut slot).
-__global__ __launch_bounds__(256) void rc_b2_items_kernel(const uint64_t *__restrict__ ptrs,
-                                                          const uint64_t *__restrict__ cut_base,
-                                                          const uint64_t *__restrict__ cuts,
-                                                          const int64_t *__restrict__ counts,
-                                                          const uint64_t *__restrict__ chunk_off,
-                                                          B2Item *__restrict__ items) {
-    const uint64_t i = blockIdx.x;
-    const int64_t cnt = counts[i];
-    const uint64_t base = cut_base[i], o = chunk_off[i], p = ptrs[i];
-    for (int64_t k = threadIdx.x; k < cnt; k += blockDim.x) {
-        const uint64_t start = k ? cuts[base + k - 1] : 0, end = cuts[base + k];
-        items[o + k] = B2Item{p + start, end - start, base + k};
+struct ChunkLists {
+    const uint64_t *ptrs, *cut_base, *cuts;
+    const int64_t *counts;
+    uint64_t n, spw;  // streams, streams per workgroup
+};
+
+// Pass 2: per workgroup (a run of spw streams) a histogram of its chunks' buckets, stored
+// bucket-major: hist[b * G + g].
+__global__ __launch_bounds__(256) void rc_b2_hist_kernel(ChunkLists c, uint32_t *__restrict__ hist) {
+    __shared__ uint32_t h[kB2Buckets];
+    for (int b = threadIdx.x; b < kB2Buckets; b += 256) h[b] = 0;
+    __syncthreads();
+    const uint64_t s0 = blockIdx.x * c.spw, s1 = s0 + c.spw < c.n ? s0 + c.spw : c.n;
+    for (uint64_t s = s0; s < s1; ++s) {
+        const int64_t cnt = c.counts[s];
+        const uint64_t *e = c.cuts + c.cut_base[s];
+        for (int64_t k = threadIdx.x; k < cnt; k += 256)
+            atomicAdd(&h[len_bucket(e[k] - (k ? e[k - 1] : 0))], 1u);
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < kB2Buckets; b += 256) hist[uint64_t(b) * gridDim.x + blockIdx.x] = h[b];
+}
+
+// Pass 3 (one workgroup): exclusive scan of hist in place (bucket-major = longest first).
+__global__ __launch_bounds__(1024) void rc_b2_hscan_kernel(uint32_t *__restrict__ hist, uint64_t m) {
+    __shared__ uint64_t part[1024];
+    const uint64_t per = (m + 1023) / 1024;
+    const uint64_t lo = threadIdx.x * per, hi = lo + per < m ? lo + per : m;
+    uint64_t s = 0;
+    for (uint64_t i = lo; i < hi; ++i) s += hist[i];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+        const uint64_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+        __syncthreads();
+        part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint64_t acc = part[threadIdx.x] - s;
+    for (uint64_t i = lo; i < hi; ++i) {
+        const uint32_t v = hist[i];
+        hist[i] = static_cast<uint32_t>(acc);
+        acc += v;
+    }
+}
+
+// Pass 4: scatter every chunk to its sorted position (start address, length, cut slot).
+__global__ __launch_bounds__(256) void rc_b2_scatter_kernel(ChunkLists c,
+                                                            const uint32_t *__restrict__ off,
+                                                            B2Item *__restrict__ items) {
+    __shared__ uint32_t cur[kB2Buckets];
+    for (int b = threadIdx.x; b < kB2Buckets; b += 256) cur[b] = off[uint64_t(b) * gridDim.x + blockIdx.x];
+    __syncthreads();
+    const uint64_t s0 = blockIdx.x * c.spw, s1 = s0 + c.spw < c.n ? s0 + c.spw : c.n;
+    for (uint64_t s = s0; s < s1; ++s) {
+        const int64_t cnt = c.counts[s];
+        const uint64_t base = c.cut_base[s], p = c.ptrs[s];
+        const uint64_t *e = c.cuts + base;
+        for (int64_t k = threadIdx.x; k < cnt; k += 256) {
+            const uint64_t start = k ? e[k - 1] : 0, len = e[k] - start;
+            const uint32_t pos = atomicAdd(&cur[len_bucket(len)], 1u);
+            items[pos] = B2Item{p + start, len, base + k};
+        }
     }
 }
 
@@ -343,14 +437,19 @@ int rc_b2_launch_items(const B2Item *d_items, uint64_t n, uint32_t outlen, uint8
 
 int rc_b2_launch_chunks(uint64_t n, const uint64_t *d_ptrs, const uint64_t *d_cut_base,
                         const uint64_t *d_cuts, const int64_t *d_counts, uint64_t *d_chunk_off,
-                        B2Item *d_items, uint64_t items_cap, uint32_t outlen, uint8_t *d_out,
-                        hipStream_t stream) {
+                        uint32_t *d_hist, B2Item *d_items, uint64_t items_cap, uint32_t outlen,
+                        uint8_t *d_out, hipStream_t stream) {
     if (!n) return 0;
     rc_b2_scan_kernel<<<1, 1024, 0, stream>>>(d_counts, n, d_chunk_off);
     if (b2_status("rc_b2_scan_kernel")) return 1;
-    rc_b2_items_kernel<<<static_cast<unsigned>(n), 256, 0, stream>>>(d_ptrs, d_cut_base, d_cuts,
-                                                                    d_counts, d_chunk_off, d_items);
-    if (b2_status("rc_b2_items_kernel")) return 1;
+    const ChunkLists c{d_ptrs, d_cut_base, d_cuts, d_counts, n, rc_b2_streams_per_group(n)};
+    const unsigned groups = static_cast<unsigned>((n + c.spw - 1) / c.spw);
+    rc_b2_hist_kernel<<<groups, 256, 0, stream>>>(c, d_hist);
+    if (b2_status("rc_b2_hist_kernel")) return 1;
+    rc_b2_hscan_kernel<<<1, 1024, 0, stream>>>(d_hist, uint64_t(kB2Buckets) * groups);
+    if (b2_status("rc_b2_hscan_kernel")) return 1;
+    rc_b2_scatter_kernel<<<groups, 256, 0, stream>>>(c, d_hist, d_items);
+    if (b2_status("rc_b2_scatter_kernel")) return 1;
     rc_b2_kernel<<<b2_grid(items_cap), kB2Threads, 0, stream>>>(d_items, d_chunk_off + n, 0,
                                                                 outlen, d_out);
     return b2_status("rc_b2_kernel");

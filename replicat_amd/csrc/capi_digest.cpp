@@ -146,6 +146,8 @@ int enqueue_items(rc_hasher *h, uint64_t n, const uint8_t *const *d_ptrs, const 
     if (int rc = w->d_stage.ensure(bytes)) return rc;
     B2Item *it = static_cast<B2Item *>(w->h_stage.p);
     for (uint64_t i = 0; i < n; ++i) it[i] = B2Item{reinterpret_cast<uint64_t>(d_ptrs[i]), lens[i], i};
+    // longest first: the kernel deals items round-robin (see blake2b.hip)
+    std::stable_sort(it, it + n, [](const B2Item &x, const B2Item &y) { return x.len > y.len; });
     RC_HIP_TRY(hipMemcpyAsync(w->d_stage.p, w->h_stage.p, bytes, hipMemcpyHostToDevice, st));
     std::array<hipEvent_t, 2> ev{};
     if (int rc = timing_begin(h, st, ev)) return rc;
@@ -174,10 +176,11 @@ int rc_hasher_enqueue_chunks(rc_hasher *h, uint64_t n, const uint8_t *const *d_p
     Guard g(h->device);
     Workspace *w = nullptr;
     if (int rc = acquire(h, w)) return rc;
-    // staging: ptr[n] cut_base[n] | device also: chunk_off[n+1]
+    // staging: ptr[n] cut_base[n] | device also: chunk_off[n+1], the sort histogram
     const size_t up = 2 * n * sizeof(uint64_t);
+    const size_t hist_off = up + (n + 1) * sizeof(uint64_t);
     if (int rc = w->h_stage.ensure(up)) return rc;
-    if (int rc = w->d_stage.ensure(up + (n + 1) * sizeof(uint64_t))) return rc;
+    if (int rc = w->d_stage.ensure(hist_off + rc_b2_hist_words(n) * sizeof(uint32_t))) return rc;
     if (int rc = w->d_items.ensure(std::max<uint64_t>(total_cap, 1) * sizeof(B2Item))) return rc;
     uint64_t *u = static_cast<uint64_t *>(w->h_stage.p);
     for (uint64_t i = 0; i < n; ++i) {
@@ -189,7 +192,8 @@ int rc_hasher_enqueue_chunks(rc_hasher *h, uint64_t n, const uint8_t *const *d_p
     uint64_t *chunk_off = static_cast<uint64_t *>(w->d_stage.p) + 2 * n;
     std::array<hipEvent_t, 2> ev{};
     if (int rc = timing_begin(h, st, ev)) return rc;
-    if (rc_b2_launch_chunks(n, d, d + n, d_cuts, d_counts, chunk_off,
+    uint32_t *hist = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(w->d_stage.p) + hist_off);
+    if (rc_b2_launch_chunks(n, d, d + n, d_cuts, d_counts, chunk_off, hist,
                             static_cast<B2Item *>(w->d_items.p), total_cap, h->digest_size, d_out,
                             st))
         return rc_fail(RC_ERR_HIP, "%s", rc_b2_launch_error());

@@ -10,6 +10,9 @@ struct B2Item {
 
 constexpr int kB2Threads = 256;       // 4 waves, 64 quads per workgroup
 constexpr uint64_t kB2MaxGroups = 512;  // 2 waves per SIMD on 256 CUs; items beyond loop
+constexpr uint64_t kB2OneWaveGroups = 256;   // one wave per SIMD
+constexpr uint64_t kB2TwoWaveItems = 65536;  // from this many items on, two waves per SIMD
+constexpr int kB2Buckets = 256;       // length classes of the longest-first work list
 constexpr uint64_t kB2Slot = 64;      // bytes per digest slot (BLAKE2b's largest digest)
 
 const char *rc_b2_launch_error(void);
@@ -18,10 +21,17 @@ const char *rc_b2_launch_error(void);
 int rc_b2_launch_items(const B2Item *d_items, uint64_t n, uint32_t outlen, uint8_t *d_out,
                        hipStream_t stream);
 
+// Streams per workgroup of the work-list passes, and the size (u32 words) of their histogram.
+inline uint64_t rc_b2_streams_per_group(uint64_t n) { return n ? (n + 1023) / 1024 : 1; }
+inline uint64_t rc_b2_hist_words(uint64_t n) {
+    const uint64_t spw = rc_b2_streams_per_group(n);
+    return uint64_t(kB2Buckets) * ((n + spw - 1) / spw + 1);
+}
+
 // Digests of the chunks of n streams as rc_chunk_device wrote them: d_cuts at d_cut_base[i],
-// d_counts[i] chunks.  d_chunk_off has n + 1 entries; d_items holds items_cap (>= sum of
-// counts) entries.
+// d_counts[i] chunks.  d_chunk_off has n + 1 entries, d_hist rc_b2_hist_words(n); d_items holds
+// items_cap (>= sum of counts) entries.  The work list is sorted longest first on the device.
 int rc_b2_launch_chunks(uint64_t n, const uint64_t *d_ptrs, const uint64_t *d_cut_base,
                         const uint64_t *d_cuts, const int64_t *d_counts, uint64_t *d_chunk_off,
-                        B2Item *d_items, uint64_t items_cap, uint32_t outlen, uint8_t *d_out,
-                        hipStream_t stream);
+                        uint32_t *d_hist, B2Item *d_items, uint64_t items_cap, uint32_t outlen,
+                        uint8_t *d_out, hipStream_t stream);
