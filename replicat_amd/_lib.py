@@ -17,6 +17,7 @@ RC_ERR_KEY_LENGTH = 1
 RC_ERR_MIN_GT_MAX = 2
 RC_ERR_BAD_KEY = 3
 RC_ERR_DIGEST_SIZE = 4
+RC_ERR_B2_PARAM = 5
 RC_ERR_ARGUMENT = 10
 RC_ERR_ALIGN = 11
 RC_ERR_HIP = 12
@@ -58,6 +59,8 @@ SIGNATURES = {
     'rc_blake2b_host': (_int, [_p, _u64, _p, _p, _p]),
     'rc_blake2b_chunks': (_int, [_p, _p, _u64, _p, _p, _p, _p, _p, _p]),
     'rc_chunk_digest_host': (_int, [_p, _p, _u64, _p, _p, _p, _u32, _p, _p, _p]),
+    'rc_blake2b_state_init': (_int, [_u32, _p, _u32, _p, _u32, _p, _u32, _p]),
+    'rc_blake2b_update_device': (_int, [_p, _u64, _p, _p, _p, _p, _p, _p]),
     'rc_blake2b_timing_enable': (_int, [_p, _int]),
     'rc_blake2b_timing_read': (_int, [_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_u64)]),
 }
@@ -110,7 +113,8 @@ def check(code):
     if code == RC_OK:
         return
     msg = last_error()
-    if code in (RC_ERR_KEY_LENGTH, RC_ERR_MIN_GT_MAX, RC_ERR_BAD_KEY, RC_ERR_DIGEST_SIZE):
+    if code in (RC_ERR_KEY_LENGTH, RC_ERR_MIN_GT_MAX, RC_ERR_BAD_KEY, RC_ERR_DIGEST_SIZE,
+                RC_ERR_B2_PARAM):
         raise ValueError(msg)
     if code == RC_ERR_NO_DEVICE:
         raise ChunkerUnavailable(msg)

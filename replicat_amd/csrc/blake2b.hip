@@ -178,6 +178,105 @@ __device__ __forceinline__ uint32_t byte_mask(int64_t valid) {
 
 }  // namespace
 
+namespace {
+
+// Lane q's message pointers and constants; qb is the quad's 128-byte block in LDS.
+__device__ __forceinline__ LaneCtx make_ctx(int q, uint64_t *qb) {
+    LaneCtx cx;
+#pragma unroll
+    for (int r = 0; r < 10; ++r)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) cx.mp[r][k] = qb + ((sigma_pack(r, k) >> (4 * q)) & 15u);
+    cx.iv_c = q == 0 ? kIV[0] : q == 1 ? kIV[1] : q == 2 ? kIV[2] : kIV[3];
+    cx.iv_d = q == 0 ? kIV[4] : q == 1 ? kIV[5] : q == 2 ? kIV[6] : kIV[7];
+    cx.t_mask = q == 0 ? ~0ull : 0ull;
+    cx.f_mask = q == 2 ? ~0ull : 0ull;
+    return cx;
+}
+
+// Compress blocks 0 .. nfull-1 of a message (non-final; counter t0 + 128 (b + 1)).  a4/sh: the
+// lane's 4-aligned base (p + 32 q rounded down) and its byte shift.
+__device__ __forceinline__ void body_blocks(uint64_t &h0, uint64_t &h1, const LaneCtx &cx,
+                                            uint64_t *qb, int q, gbytes a4, uint32_t sh,
+                                            uint64_t nfull, uint64_t t0) {
+    // blocks b >= nfull are not loaded by the loop: clamp to block 0 (always readable when
+    // nfull > 0) so that every iteration issues the same loads
+    auto blk = [&](uint64_t b) { return a4 + 128 * (b < nfull ? b : 0); };
+    Raw A, B;
+    if (nfull) {
+        A = load_raw(blk(0));
+        B = load_raw(blk(1));
+    }
+    // two blocks per iteration with fixed register roles: copying A = B would make the
+    // compiler wait for B's loads (vmcnt(0)) and collapse the prefetch distance
+    uint64_t b = 0;
+    for (; b + 2 <= nfull; b += 2) {
+        stage(qb, q, A, sh);
+        A = load_raw(blk(b + 2));
+        compress(h0, h1, cx, t0 + (b + 1) * 128, false);
+        stage(qb, q, B, sh);
+        B = load_raw(blk(b + 3));
+        compress(h0, h1, cx, t0 + (b + 2) * 128, false);
+    }
+    if (b < nfull) {  // odd count: A holds block b
+        stage(qb, q, A, sh);
+        compress(h0, h1, cx, t0 + (b + 1) * 128, false);
+    }
+}
+
+// Stage block nfull -- the last 1..128 bytes of a len-byte message at p (0 bytes only for an
+// empty one) -- into qb, zero past the message end.  Nothing beyond its last dword is read.
+__device__ __forceinline__ void stage_last(uint64_t *qb, int q, gbytes p, gbytes a4, uint32_t sh,
+                                           uint64_t nfull, uint64_t len) {
+    const int64_t rem = static_cast<int64_t>(len - nfull * 128);
+    Raw F;
+    if (len) {
+        const uintptr_t last = (reinterpret_cast<uintptr_t>(p) + len - 1) & ~uintptr_t(3);
+        const uintptr_t f4 = reinterpret_cast<uintptr_t>(a4) + 128 * nfull;
+        uint32_t w[9];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+            uintptr_t a = f4 + 4 * i;
+            a = a < last ? a : last;
+            w[i] = *reinterpret_cast<const GLOBAL uint32_t *>(a);
+        }
+        F.x = u32x4{w[0], w[1], w[2], w[3]};
+        F.y = u32x4{w[4], w[5], w[6], w[7]};
+        F.z = w[8];
+    } else {
+        F.x = F.y = u32x4{0u, 0u, 0u, 0u};
+        F.z = 0;
+    }
+    // funnel, then zero the bytes at or past the message end
+    const uint32_t sb = sh * 8;
+    const int64_t v0 = rem - 32 * q;
+    u32x4 o0, o1;
+    o0.x = __builtin_amdgcn_alignbit(F.x.y, F.x.x, sb) & byte_mask(v0);
+    o0.y = __builtin_amdgcn_alignbit(F.x.z, F.x.y, sb) & byte_mask(v0 - 4);
+    o0.z = __builtin_amdgcn_alignbit(F.x.w, F.x.z, sb) & byte_mask(v0 - 8);
+    o0.w = __builtin_amdgcn_alignbit(F.y.x, F.x.w, sb) & byte_mask(v0 - 12);
+    o1.x = __builtin_amdgcn_alignbit(F.y.y, F.y.x, sb) & byte_mask(v0 - 16);
+    o1.y = __builtin_amdgcn_alignbit(F.y.z, F.y.y, sb) & byte_mask(v0 - 20);
+    o1.z = __builtin_amdgcn_alignbit(F.y.w, F.y.z, sb) & byte_mask(v0 - 24);
+    o1.w = __builtin_amdgcn_alignbit(F.z, F.y.w, sb) & byte_mask(v0 - 28);
+    *reinterpret_cast<u32x4 *>(qb + 4 * q) = o0;
+    *reinterpret_cast<u32x4 *>(qb + 4 * q + 2) = o1;
+}
+
+// digest bytes [8q, 8q+8) = h[q] and [32+8q, 40+8q) = h[q+4]; bytes >= outlen are zero
+__device__ __forceinline__ void write_digest(uint8_t *slot, int q, uint64_t h0, uint64_t h1,
+                                             uint32_t outlen) {
+    auto keep = [&](uint64_t h, int byte0) -> uint64_t {
+        const int v = static_cast<int>(outlen) - byte0;
+        return v >= 8 ? h : v <= 0 ? 0ull : h & ((1ull << (8 * v)) - 1);
+    };
+    uint64_t *o = reinterpret_cast<uint64_t *>(slot);
+    o[q] = keep(h0, 8 * q);
+    o[4 + q] = keep(h1, 32 + 8 * q);
+}
+
+}  // namespace
+
 // One quad per chunk; a workgroup is kB2Threads / 4 quads.  Items g = quad, quad + Q, ...
 __global__ __launch_bounds__(kB2Threads) void rc_b2_kernel(const B2Item *__restrict__ items,
                                                            const uint64_t *__restrict__ d_total,
@@ -188,15 +287,7 @@ __global__ __launch_bounds__(kB2Threads) void rc_b2_kernel(const B2Item *__restr
     const int quad = threadIdx.x >> 2;
     uint64_t *qb = blocks + quad * 16;
 
-    LaneCtx cx;
-#pragma unroll
-    for (int r = 0; r < 10; ++r)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) cx.mp[r][k] = qb + ((sigma_pack(r, k) >> (4 * q)) & 15u);
-    cx.iv_c = q == 0 ? kIV[0] : q == 1 ? kIV[1] : q == 2 ? kIV[2] : kIV[3];
-    cx.iv_d = q == 0 ? kIV[4] : q == 1 ? kIV[5] : q == 2 ? kIV[6] : kIV[7];
-    cx.t_mask = q == 0 ? ~0ull : 0ull;
-    cx.f_mask = q == 2 ? ~0ull : 0ull;
+    const LaneCtx cx = make_ctx(q, qb);
     const uint64_t h0_init = (q == 0 ? kIV[0] ^ (0x01010000ull | outlen) : cx.iv_c);
     const uint64_t h1_init = cx.iv_d;
 
@@ -225,79 +316,90 @@ __global__ __launch_bounds__(kB2Threads) void rc_b2_kernel(const B2Item *__restr
         const uint64_t len = it.len;
         uint64_t h0 = h0_init, h1 = h1_init;
         const uint64_t nfull = len ? (len - 1) / 128 : 0;  // non-final blocks
-
         // lane base of block b: p + 128 b + 32 q, funnelled from its 4-aligned dword
         gbytes lb = p + 32 * q;
         const uint32_t sh = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(lb) & 3);
         gbytes a4 = lb - sh;
-        // blocks b >= nfull are not loaded by the loop: clamp to block 0 (always readable when
-        // nfull > 0) so that every iteration issues the same loads
-        auto blk = [&](uint64_t b) { return a4 + 128 * (b < nfull ? b : 0); };
-        Raw A, B;
-        if (nfull) {
-            A = load_raw(blk(0));
-            B = load_raw(blk(1));
+        body_blocks(h0, h1, cx, qb, q, a4, sh, nfull, 0);
+        stage_last(qb, q, p, a4, sh, nfull, len);
+        compress(h0, h1, cx, len, true);
+        write_digest(out + it.slot * kB2Slot, q, h0, h1, outlen);
+    }
+}
+
+// Incremental / keyed BLAKE2b: one quad per (state, buffer) item.  The state holds the chaining
+// value, the byte counter and the last 1..128 message bytes not yet compressed (BLAKE2b may
+// compress a block only once it knows whether the block is the last).  A keyed state starts
+// with the zero-padded key as its pending block (RFC 7693 §3.3), so a keyed or salted hash is
+// the same walk.  Non-final items write the state back; final items write the digest only.
+__global__ __launch_bounds__(kB2Threads) void rc_b2_update_kernel(const B2UItem *__restrict__ items,
+                                                                  uint64_t total,
+                                                                  uint8_t *__restrict__ out) {
+    __shared__ uint64_t blocks[kB2Threads / 4 * 16];
+    const int q = threadIdx.x & 3;
+    const int quad = threadIdx.x >> 2;
+    uint64_t *qb = blocks + quad * 16;
+    uint8_t *qbb = reinterpret_cast<uint8_t *>(qb);
+    const LaneCtx cx = make_ctx(q, qb);
+
+    const uint64_t nq = uint64_t(gridDim.x) * (kB2Threads / 4);
+    for (uint64_t g = uint64_t(blockIdx.x) * (kB2Threads / 4) + quad; g < total; g += nq) {
+        const B2UItem it = items[g];
+        rc_blake2b_state *st = reinterpret_cast<rc_blake2b_state *>(it.state);
+        uint64_t h0 = st->h[q], h1 = st->h[q + 4];
+        uint64_t t = st->t;
+        const uint64_t buflen = st->buflen;
+        const uint32_t outlen = st->digest_size;
+        gbytes p = reinterpret_cast<gbytes>(it.ptr);
+        uint64_t len = it.len;
+        const bool final = it.final != 0;
+        const uint64_t tot = buflen + len;
+        if (!final && tot <= 128) {  // still one pending block: append
+            for (uint64_t j = q; j < len; j += 4) st->buf[buflen + j] = p[j];
+            if (q == 0) st->buflen = tot;
+            continue;
         }
-        // two blocks per iteration with fixed register roles: copying A = B would make the
-        // compiler wait for B's loads (vmcnt(0)) and collapse the prefetch distance
-        uint64_t b = 0;
-        for (; b + 2 <= nfull; b += 2) {
-            stage(qb, q, A, sh);
-            A = load_raw(blk(b + 2));
-            compress(h0, h1, cx, (b + 1) * 128, false);
-            stage(qb, q, B, sh);
-            B = load_raw(blk(b + 3));
-            compress(h0, h1, cx, (b + 2) * 128, false);
-        }
-        if (b < nfull) {  // odd count: A holds block b
-            stage(qb, q, A, sh);
-            compress(h0, h1, cx, (b + 1) * 128, false);
-        }
-        // final block: rem = 1..128 bytes (0 only for an empty message)
-        {
-            const int64_t rem = static_cast<int64_t>(len - nfull * 128);
-            Raw F;
-            if (len) {
-                const uintptr_t last = (reinterpret_cast<uintptr_t>(p) + len - 1) & ~uintptr_t(3);
-                const uintptr_t f4 = reinterpret_cast<uintptr_t>(a4) + 128 * nfull;
-                uint32_t w[9];
-#pragma unroll
-                for (int i = 0; i < 9; ++i) {
-                    uintptr_t a = f4 + 4 * i;
-                    a = a < last ? a : last;
-                    w[i] = *reinterpret_cast<const GLOBAL uint32_t *>(a);
-                }
-                F.x = u32x4{w[0], w[1], w[2], w[3]};
-                F.y = u32x4{w[4], w[5], w[6], w[7]};
-                F.z = w[8];
-            } else {
-                F.x = F.y = u32x4{0u, 0u, 0u, 0u};
-                F.z = 0;
+        if (buflen) {  // pending bytes + the first bytes of p form the next block
+#pragma unroll 4
+            for (int i = 0; i < 32; ++i) {
+                const uint64_t j = 32 * q + i;
+                uint8_t v = 0;
+                if (j < buflen)
+                    v = st->buf[j];
+                else if (j - buflen < len)
+                    v = p[j - buflen];
+                qbb[j] = v;
             }
-            // funnel, then zero the bytes at or past the chunk end
-            const uint32_t sb = sh * 8;
-            const int64_t v0 = rem - 32 * q;
-            u32x4 o0, o1;
-            o0.x = __builtin_amdgcn_alignbit(F.x.y, F.x.x, sb) & byte_mask(v0);
-            o0.y = __builtin_amdgcn_alignbit(F.x.z, F.x.y, sb) & byte_mask(v0 - 4);
-            o0.z = __builtin_amdgcn_alignbit(F.x.w, F.x.z, sb) & byte_mask(v0 - 8);
-            o0.w = __builtin_amdgcn_alignbit(F.y.x, F.x.w, sb) & byte_mask(v0 - 12);
-            o1.x = __builtin_amdgcn_alignbit(F.y.y, F.y.x, sb) & byte_mask(v0 - 16);
-            o1.y = __builtin_amdgcn_alignbit(F.y.z, F.y.y, sb) & byte_mask(v0 - 20);
-            o1.z = __builtin_amdgcn_alignbit(F.y.w, F.y.z, sb) & byte_mask(v0 - 24);
-            o1.w = __builtin_amdgcn_alignbit(F.z, F.y.w, sb) & byte_mask(v0 - 28);
-            *reinterpret_cast<u32x4 *>(qb + 4 * q) = o0;
-            *reinterpret_cast<u32x4 *>(qb + 4 * q + 2) = o1;
-            compress(h0, h1, cx, len, true);
+            if (tot <= 128) {  // final and short: this is the last block
+                compress(h0, h1, cx, t + tot, true);
+                write_digest(out + it.slot * kB2Slot, q, h0, h1, outlen);
+                continue;
+            }
+            compress(h0, h1, cx, t + 128, false);
+            t += 128;
+            p += 128 - buflen;
+            len -= 128 - buflen;
         }
-        // digest bytes [8q, 8q+8) = h[q] and [32+8q, 40+8q) = h[q+4]; bytes >= outlen are zero
-        auto keep = [&](uint64_t h, int byte0) -> uint64_t {
-            const int v = static_cast<int>(outlen) - byte0;
-            return v >= 8 ? h : v <= 0 ? 0ull : h & ((1ull << (8 * v)) - 1);
-        };
-        uint64_t *o = reinterpret_cast<uint64_t *>(out + it.slot * kB2Slot);
-        o[q] = keep(h0, 8 * q);
-        o[4 + q] = keep(h1, 32 + 8 * q);
+        const uint64_t nfull = len ? (len - 1) / 128 : 0;
+        gbytes lb = p + 32 * q;
+        const uint32_t sh = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(lb) & 3);
+        gbytes a4 = lb - sh;
+        body_blocks(h0, h1, cx, qb, q, a4, sh, nfull, t);
+        stage_last(qb, q, p, a4, sh, nfull, len);
+        if (final) {
+            compress(h0, h1, cx, t + len, true);
+            write_digest(out + it.slot * kB2Slot, q, h0, h1, outlen);
+        } else {  // keep the last 1..128 bytes pending
+            u32x4 *dst = reinterpret_cast<u32x4 *>(st->buf + 32 * q);
+            dst[0] = *reinterpret_cast<const u32x4 *>(qb + 4 * q);
+            dst[1] = *reinterpret_cast<const u32x4 *>(qb + 4 * q + 2);
+            st->h[q] = h0;
+            st->h[q + 4] = h1;
+            if (q == 0) {
+                st->t = t + 128 * nfull;
+                st->buflen = len - 128 * nfull;
+            }
+        }
     }
 }
 
@@ -453,4 +555,10 @@ int rc_b2_launch_chunks(uint64_t n, const uint64_t *d_ptrs, const uint64_t *d_cu
     rc_b2_kernel<<<b2_grid(items_cap), kB2Threads, 0, stream>>>(d_items, d_chunk_off + n, 0,
                                                                 outlen, d_out);
     return b2_status("rc_b2_kernel");
+}
+
+int rc_b2_launch_update(const B2UItem *d_items, uint64_t n, uint8_t *d_out, hipStream_t stream) {
+    if (!n) return 0;
+    rc_b2_update_kernel<<<b2_grid(n), kB2Threads, 0, stream>>>(d_items, n, d_out);
+    return b2_status("rc_b2_update_kernel");
 }

@@ -16,6 +16,8 @@
 #include "capi_internal.h"
 #include "digest_kernels.h"
 
+static_assert(sizeof(rc_blake2b_state) == 256, "rc_blake2b_state is a 256-byte device record");
+
 namespace {
 
 struct DevMem {
@@ -152,6 +154,29 @@ int enqueue_items(rc_hasher *h, uint64_t n, const uint8_t *const *d_ptrs, const 
     std::array<hipEvent_t, 2> ev{};
     if (int rc = timing_begin(h, st, ev)) return rc;
     if (rc_b2_launch_items(static_cast<const B2Item *>(w->d_stage.p), n, h->digest_size, d_out, st))
+        return rc_fail(RC_ERR_HIP, "%s", rc_b2_launch_error());
+    if (int rc = timing_end(h, st, ev)) return rc;
+    return finish(h, *w, st);
+}
+
+// incremental updates: items built on the host
+int enqueue_update(rc_hasher *h, uint64_t n, rc_blake2b_state *const *d_states,
+                   const uint8_t *const *d_ptrs, const uint64_t *lens, const uint8_t *finals,
+                   uint8_t *d_out, hipStream_t st) {
+    Workspace *w = nullptr;
+    if (int rc = acquire(h, w)) return rc;
+    const size_t bytes = n * sizeof(B2UItem);
+    if (int rc = w->h_stage.ensure(bytes)) return rc;
+    if (int rc = w->d_stage.ensure(bytes)) return rc;
+    B2UItem *it = static_cast<B2UItem *>(w->h_stage.p);
+    for (uint64_t i = 0; i < n; ++i)
+        it[i] = B2UItem{reinterpret_cast<uint64_t>(d_ptrs[i]), lens[i], i,
+                        reinterpret_cast<uint64_t>(d_states[i]), finals && finals[i] ? 1u : 0u, 0u};
+    std::stable_sort(it, it + n, [](const B2UItem &x, const B2UItem &y) { return x.len > y.len; });
+    RC_HIP_TRY(hipMemcpyAsync(w->d_stage.p, w->h_stage.p, bytes, hipMemcpyHostToDevice, st));
+    std::array<hipEvent_t, 2> ev{};
+    if (int rc = timing_begin(h, st, ev)) return rc;
+    if (rc_b2_launch_update(static_cast<const B2UItem *>(w->d_stage.p), n, d_out, st))
         return rc_fail(RC_ERR_HIP, "%s", rc_b2_launch_error());
     if (int rc = timing_end(h, st, ev)) return rc;
     return finish(h, *w, st);
@@ -303,6 +328,65 @@ int rc_blake2b_chunks(rc_hasher *h, const rc_chunker *layout, uint64_t n,
     }
     return rc_hasher_enqueue_chunks(h, n, d_streams, base.data(), d_cuts, d_counts, total, d_digests,
                                     static_cast<hipStream_t>(hip_stream));
+}
+
+int rc_blake2b_state_init(uint32_t digest_size, const uint8_t *key, uint32_t keylen,
+                          const uint8_t *salt, uint32_t saltlen, const uint8_t *person,
+                          uint32_t personlen, rc_blake2b_state *out) {
+    static const uint64_t iv[8] = {0x6a09e667f3bcc908ull, 0xbb67ae8584caa73bull,
+                                   0x3c6ef372fe94f82bull, 0xa54ff53a5f1d36f1ull,
+                                   0x510e527fade682d1ull, 0x9b05688c2b3e6c1full,
+                                   0x1f83d9abfb41bd6bull, 0x5be0cd19137e2179ull};
+    if (!out) return rc_fail(RC_ERR_ARGUMENT, "null state");
+    if (digest_size < 1 || digest_size > 64)
+        return rc_fail(RC_ERR_DIGEST_SIZE, "digest_size must be between 1 and 64 bytes");
+    if (keylen > 64) return rc_fail(RC_ERR_B2_PARAM, "maximum key length is 64 bytes");
+    if (saltlen > 16) return rc_fail(RC_ERR_B2_PARAM, "maximum salt length is 16 bytes");
+    if (personlen > 16) return rc_fail(RC_ERR_B2_PARAM, "maximum person length is 16 bytes");
+    if ((keylen && !key) || (saltlen && !salt) || (personlen && !person))
+        return rc_fail(RC_ERR_ARGUMENT, "null key / salt / person");
+    // parameter block (RFC 7693 §2.8): digest length, key length, fanout 1, depth 1; salt at
+    // byte 32, personalisation at byte 48; everything else zero (sequential mode)
+    uint8_t pb[64] = {};
+    pb[0] = static_cast<uint8_t>(digest_size);
+    pb[1] = static_cast<uint8_t>(keylen);
+    pb[2] = 1;
+    pb[3] = 1;
+    if (saltlen) std::memcpy(pb + 32, salt, saltlen);
+    if (personlen) std::memcpy(pb + 48, person, personlen);
+    std::memset(out, 0, sizeof *out);
+    for (int i = 0; i < 8; ++i) {
+        uint64_t w;
+        std::memcpy(&w, pb + 8 * i, 8);  // little-endian host (x86-64)
+        out->h[i] = iv[i] ^ w;
+    }
+    out->digest_size = digest_size;
+    if (keylen) {  // the key, zero-padded to a block, is the first (pending) block (§3.3)
+        std::memcpy(out->buf, key, keylen);
+        out->buflen = 128;
+    }
+    return RC_OK;
+}
+
+int rc_blake2b_update_device(rc_hasher *h, uint64_t n, rc_blake2b_state *const *d_states,
+                             const uint8_t *const *d_ptrs, const uint64_t *lens,
+                             const uint8_t *finals, uint8_t *d_out, void *hip_stream) {
+    if (!h) return rc_fail(RC_ERR_ARGUMENT, "null hasher");
+    if (n == 0) return RC_OK;
+    if (!d_states) return rc_fail(RC_ERR_ARGUMENT, "null state array");
+    if (int rc = check_buffers(n, d_ptrs, lens)) return rc;
+    bool any_final = false;
+    for (uint64_t i = 0; i < n; ++i) {
+        if (!d_states[i] || (reinterpret_cast<uintptr_t>(d_states[i]) & 15))
+            return rc_fail(RC_ERR_ARGUMENT, "state %llu: null or not 16-byte aligned",
+                           (unsigned long long)i);
+        any_final = any_final || (finals && finals[i]);
+    }
+    if (any_final && !d_out) return rc_fail(RC_ERR_ARGUMENT, "null output");
+    std::lock_guard<std::mutex> lock(h->mu);
+    Guard g(h->device);
+    return enqueue_update(h, n, d_states, d_ptrs, lens, finals, d_out,
+                          static_cast<hipStream_t>(hip_stream));
 }
 
 int rc_blake2b_timing_enable(rc_hasher *h, int enable) {

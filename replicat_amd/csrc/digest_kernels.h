@@ -3,9 +3,17 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/replicat_digest.h"
+
 // One message to hash: device address, length in bytes, output slot (digest at out + 64 * slot).
 struct B2Item {
     uint64_t ptr, len, slot;
+};
+
+// One (state, buffer) pair of an incremental / keyed update: state is a device rc_blake2b_state.
+struct B2UItem {
+    uint64_t ptr, len, slot, state;
+    uint32_t final, pad;
 };
 
 constexpr int kB2Threads = 256;       // 4 waves, 64 quads per workgroup
@@ -20,6 +28,9 @@ const char *rc_b2_launch_error(void);
 // Digests of n items (host-built work list, already on the device).
 int rc_b2_launch_items(const B2Item *d_items, uint64_t n, uint32_t outlen, uint8_t *d_out,
                        hipStream_t stream);
+
+// Incremental updates of n (state, buffer) items; finals write the digest at d_out + 64 * slot.
+int rc_b2_launch_update(const B2UItem *d_items, uint64_t n, uint8_t *d_out, hipStream_t stream);
 
 // Streams per workgroup of the work-list passes, and the size (u32 words) of their histogram.
 inline uint64_t rc_b2_streams_per_group(uint64_t n) { return n ? (n + 1023) / 1024 : 1; }

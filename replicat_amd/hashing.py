@@ -13,8 +13,17 @@ and adds the batch entry points of include/replicat_digest.h:
 * ``digest_chunks(chunker, ...)``    -- the chunks a ``GpuChunker.chunk_device`` call left in
   HBM, digested without a host round trip (digest of cut slot s at out + 64 s).
 
-The keyed uses of the adapter (KDF, MAC: adapters.py:203-221, encrypted repositories) are not
-provided.  There is no CPU fallback: without the HIP library every call raises.
+and the incremental / keyed half of the adapter over device-resident states
+(``rc_blake2b_state``, include/replicat_digest.h):
+
+* ``state_init(digest_size, key, salt, person)`` -- hashlib.blake2b's parameters, as a 256-byte
+  record to copy to the device;
+* ``update_device(states, ptrs, lens, finals, out)`` -- many HashlibIncrementalHasher.feed /
+  .digest steps (adapters.py:106-114) in one launch: per-file digests (repository.py:1433-1446),
+  the shared-subkey KDF ``derive`` (adapters.py:203-211) and ``mac`` (:217-221);
+* ``DeviceIncrementalHasher`` -- ``incremental_hasher()`` (adapters.py:227-228) itself.
+
+There is no CPU fallback: without the HIP library every call raises.
 """
 import ctypes
 
@@ -24,6 +33,31 @@ from ._lib import RC_DIGEST_SLOT, check, lib
 from .chunker import _current_device, _ptr_array
 
 SLOT = RC_DIGEST_SLOT
+STATE_BYTES = 256   # sizeof(rc_blake2b_state)
+
+
+def _bytes_arg(name, v):
+    if v is None:
+        return b''
+    try:
+        return bytes(memoryview(v))
+    except TypeError:
+        raise TypeError(f"a bytes-like object is required, not '{type(v).__name__}'") from None
+
+
+def state_init(digest_size: int = 64, *, key=b'', salt=b'', person=b'') -> bytes:
+    """hashlib.blake2b(digest_size=..., key=..., salt=..., person=...) before any data, as the
+    256-byte rc_blake2b_state record (host memory; copy it to the device to use it).  Raises
+    hashlib's ValueErrors for out-of-range sizes."""
+    if not isinstance(digest_size, int):
+        raise TypeError(f'{type(digest_size).__name__!r} object cannot be interpreted as an integer')
+    key, salt, person = (_bytes_arg(n, v) for n, v in (('key', key), ('salt', salt),
+                                                        ('person', person)))
+    out = ctypes.create_string_buffer(STATE_BYTES)
+    check(lib().rc_blake2b_state_init(digest_size if 0 <= digest_size < 1 << 32 else 0,
+                                      key or None, len(key), salt or None, len(salt),
+                                      person or None, len(person), out))
+    return out.raw
 
 
 class GpuBlake2b:
@@ -87,6 +121,18 @@ class GpuBlake2b:
                                       lens.ctypes.data, cuts_ptr, counts_ptr, out_ptr,
                                       stream or None))
 
+    def update_device(self, state_ptrs, ptrs, lens, finals, out_ptr=0, stream=0):
+        """Enqueue incremental updates (rc_blake2b_update_device): item i feeds device buffer
+        ptrs[i] into the device state state_ptrs[i]; finals[i] also writes its digest to
+        out + 64 i (the state is then left as it was)."""
+        states, ptrs, lens = _ptr_array(state_ptrs), _ptr_array(ptrs), _ptr_array(lens)
+        fin = np.ascontiguousarray(np.asarray(finals, dtype=np.uint8).reshape(-1))
+        if not (len(states) == len(ptrs) == len(lens) == len(fin)):
+            raise ValueError('states, ptrs, lens and finals differ in length')
+        check(lib().rc_blake2b_update_device(self._h, len(lens), states.ctypes.data,
+                                             ptrs.ctypes.data, lens.ctypes.data,
+                                             fin.ctypes.data, out_ptr or None, stream or None))
+
     # ---------------------------------------------------------------------- profiling
 
     def timing(self, enable: bool):
@@ -96,6 +142,38 @@ class GpuBlake2b:
         ms, n = ctypes.c_double(), ctypes.c_uint64()
         check(lib().rc_blake2b_timing_read(self._h, ctypes.byref(ms), ctypes.byref(n)))
         return ms.value, n.value
+
+
+class DeviceIncrementalHasher:
+    """``blake2b(length).incremental_hasher()`` (adapters.py:227-228; HashlibIncrementalHasher
+    :106-114) with its state in HBM: ``feed(data)`` uploads and compresses on the device,
+    ``digest()`` finalises.  Optional key / salt / person as hashlib.blake2b takes them."""
+
+    def __init__(self, hasher: 'GpuBlake2b', *, key=b'', salt=b'', person=b''):
+        import torch
+        self._hasher = hasher
+        dev = torch.device('cuda', hasher.device)
+        init = np.frombuffer(state_init(hasher.digest_size, key=key, salt=salt, person=person),
+                             dtype=np.uint8)
+        self._state = torch.from_numpy(init.copy()).to(dev)
+        self._slot = torch.zeros(SLOT, dtype=torch.uint8, device=dev)
+        self._dev = dev
+
+    def _run(self, data, final):
+        import torch
+        arr = np.frombuffer(data, dtype=np.uint8) if len(data) else np.zeros(0, np.uint8)
+        buf = torch.from_numpy(arr.copy()).to(self._dev) if arr.size else None
+        stream = torch.cuda.current_stream(self._dev).cuda_stream
+        self._hasher.update_device([self._state.data_ptr()], [buf.data_ptr() if buf is not None else 0],
+                                   [arr.size], [1 if final else 0], self._slot.data_ptr(), stream)
+        torch.cuda.current_stream(self._dev).synchronize()
+
+    def feed(self, data) -> None:
+        self._run(memoryview(data).cast('B'), False)
+
+    def digest(self) -> bytes:
+        self._run(b'', True)
+        return self._slot.cpu().numpy()[:self._hasher.digest_size].tobytes()
 
 
 def chunk_digest_host(chunker, hasher, buffers, last_piece=None, open_=False):
@@ -123,4 +201,5 @@ def chunk_digest_host(chunker, hasher, buffers, last_piece=None, open_=False):
             [digests[b:b + c, :hasher.digest_size] for b, c in zip(base, counts)])
 
 
-__all__ = ['GpuBlake2b', 'chunk_digest_host', 'SLOT']
+__all__ = ['GpuBlake2b', 'DeviceIncrementalHasher', 'chunk_digest_host', 'state_init', 'SLOT',
+           'STATE_BYTES']
