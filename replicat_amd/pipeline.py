@@ -1,0 +1,241 @@
+"""replicat's snapshot chunk producer on the device (SURVEY.md §8 f, ranks 1-3 together).
+
+What it replaces, in /root/reference/replicat/repository.py:
+
+* ``_stream_files`` (:1413-1452): files sorted by (size, path), read in 16 MiB pieces, zero
+  padding to 4 bytes between files, and a ``blake2b`` incremental hasher per file (:1433-1446);
+* ``_chunk_producer`` (:1454-1505): ``chunkify`` over that ONE stream, ``hash_digest`` of every
+  chunk (:1462), the digest -> table-index dedup map (:1464-1468), the chunk counter and
+  stream offsets (:1457-1459, :1477-1485);
+* ``_chunk_done``'s file -> chunk-range map (:1374-1411).
+
+The stream is gathered into host batches (``batch_bytes``, pinned) exactly as the batching shim
+does (replicat_amd/adapters.py): every batch but the last is chunked as an OPEN prefix (the
+reference's non-final ``next_cut`` calls), the last with its real framing, and the uncut tail
+is carried into the next batch.  Each batch is uploaded ONCE and three things run on the bytes
+in HBM: the cut chain (rc_chunk_device), the chunk digests (rc_blake2b_chunks) and the per-file
+incremental digests (rc_blake2b_update_device: each file's bytes are fed once, in the batch
+that first holds them; a file's state lives in HBM across batches).  Only cut offsets and
+digests come back -- and the chunk bytes, which replicat uploads, are sliced from the host
+batch.
+
+The dedup table and the chunk -> file range map are host bookkeeping on a few integers per
+chunk, as in the reference.  There is no CPU fallback: every digest and cut comes from the HIP
+library.
+"""
+import bisect
+import os
+from dataclasses import dataclass, field
+from typing import Dict, Iterator, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from .chunker import MAX_LENGTH, MIN_LENGTH, GpuChunker, _current_device, normalize_params
+from .hashing import SLOT, STATE_BYTES, GpuBlake2b, state_init
+from .snapshot import ALIGNMENT, PIECE, sort_files
+
+DEFAULT_BATCH = 256 << 20
+
+
+@dataclass
+class FileRecord:
+    """repository.py:1427-1432 (_SnapshotFile) plus the digest of :1445."""
+    path: str
+    stream_start: int
+    stream_end: int
+    digest: Optional[bytes] = None
+
+
+@dataclass
+class ChunkRecord:
+    """repository.py:1477-1485 (_SnapshotChunk) without the upload location."""
+    counter: int
+    stream_start: int
+    stream_end: int
+    digest: bytes
+    table_index: int
+    contents: Optional[bytes] = field(default=None, repr=False)
+
+
+@dataclass
+class SnapshotStream:
+    files: List[FileRecord]
+    chunks: List[ChunkRecord]
+    chunks_table: Dict[bytes, int]
+
+    def snapshot_files(self):
+        """The ``snapshot_files`` dict _chunk_done builds (repository.py:1374-1411): per file,
+        its chunk parts ({'range', 'index', 'counter'}) and digest (metadata not collected)."""
+        starts = [(f.stream_start, i) for i, f in enumerate(self.files)]
+        out = {}
+        for c in self.chunks:
+            point = bisect.bisect_left(starts, (c.stream_end + 1,))
+            for index in range(point - 1, -1, -1):
+                f = self.files[starts[index][1]]
+                if f.stream_end < c.stream_start:
+                    break
+                d = out.setdefault(f.path, {'path': f.path, 'chunks': [], 'digest': None})
+                d['chunks'].append({'range': [max(f.stream_start - c.stream_start, 0),
+                                              min(f.stream_end, c.stream_end) - c.stream_start],
+                                    'index': c.table_index, 'counter': c.counter})
+                if c.stream_end >= f.stream_end:
+                    d['digest'] = f.digest
+        return out
+
+
+def tagged_pieces(paths: Sequence[str], files: List[FileRecord], read=None
+                  ) -> Iterator[Tuple[bytes, int]]:
+    """repository.py:1413-1447's pieces for already-sorted paths, each with the number of files
+    known to be complete when it is yielded (data of file f: f; padding after file f: f + 1).
+    `files` receives a FileRecord when a file is opened; stream_end grows as it is read."""
+    pos = 0
+    prev = None
+    for path in paths:
+        if prev is not None:
+            pad = -(prev.stream_end - prev.stream_start) % ALIGNMENT
+            if pad:
+                pos += pad
+                yield bytes(pad), len(files)
+        f = FileRecord(path=str(path), stream_start=pos, stream_end=pos)
+        files.append(f)
+        prev = f
+        with (read(path) if read else open(path, 'rb')) as src:
+            while piece := src.read(PIECE):
+                pos += len(piece)
+                f.stream_end += len(piece)
+                yield piece, len(files) - 1
+
+
+class DeviceSnapshotProducer:
+    """Chunks, chunk digests and file digests of a snapshot's stream on one HIP device."""
+
+    def __init__(self, *, min_length: int = MIN_LENGTH, max_length: int = MAX_LENGTH,
+                 params: Optional[bytes] = None, digest_size: int = 64,
+                 batch_bytes: int = DEFAULT_BATCH, device=None, keep_contents: bool = True):
+        import torch
+        if device is None:
+            device = _current_device()
+        if min_length > max_length:
+            raise ValueError(f'Minimum length ({min_length}) is greater '
+                             f'than the maximum one ({max_length})')
+        self.device = int(device)
+        self.dev = torch.device('cuda', self.device)
+        self.chunker = GpuChunker(min_length, max_length, normalize_params(params), device=self.device)
+        self.hasher = GpuBlake2b(length=digest_size, device=self.device)
+        self.min_length, self.max_length = min_length, max_length
+        self.digest_size = digest_size
+        self.batch_bytes = max(int(batch_bytes), 2 * max_length + 16)
+        self.keep_contents = keep_contents
+        # one batch plus the carried tail (< max_length) plus one piece of overshoot
+        self.capacity = self.batch_bytes + max_length + PIECE + 64
+        self.host = torch.empty(self.capacity, dtype=torch.uint8, pin_memory=True)
+        self.dbuf = torch.empty(self.capacity, dtype=torch.uint8, device=self.dev)
+        total, caps = self.chunker.capacity([self.capacity])
+        self.cut_cap = total
+        self.d_cuts = torch.zeros(max(total, 1), dtype=torch.int64, device=self.dev)
+        self.d_count = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        self.d_digests = torch.zeros((max(total, 1), SLOT), dtype=torch.uint8, device=self.dev)
+        self._init_state = np.frombuffer(state_init(digest_size), dtype=np.uint8)
+
+    # ------------------------------------------------------------------------------ run
+
+    def run(self, paths: Sequence[os.PathLike], read=None) -> SnapshotStream:
+        import torch
+        stream = torch.cuda.current_stream(self.dev)
+        hs = stream.cuda_stream
+        files: List[FileRecord] = []
+        chunks: List[ChunkRecord] = []
+        table: Dict[bytes, int] = {}
+        states = {}              # file index -> device state (open files only)
+        finalized = 0            # files [0, finalized) have their digest
+        hnp = self.host.numpy()
+        buf_start = 0            # stream offset of host[0]
+        blen = 0                 # bytes in the batch buffer
+        fed = 0                  # host[0:fed] already fed to the file digests
+        it = tagged_pieces(sort_files(paths), files, read)
+        nxt = next(it, None)
+        while True:
+            last_start = blen
+            while nxt is not None and (blen < self.batch_bytes or blen == 0):
+                piece, _ = nxt
+                last_start = blen
+                hnp[blen:blen + len(piece)] = np.frombuffer(piece, dtype=np.uint8)
+                blen += len(piece)
+                nxt = next(it, None)
+            final = nxt is None
+            closed = len(files) if final else nxt[1]
+            # ---- device: upload, cut chain, chunk digests
+            if blen:
+                self.dbuf[:blen].copy_(self.host[:blen], non_blocking=True)
+            ptr = self.dbuf.data_ptr()
+            self.chunker.chunk_device([ptr], [blen], [last_start], self.d_cuts.data_ptr(),
+                                      self.d_count.data_ptr(), hs, open_=not final)
+            self.hasher.digest_chunks(self.chunker, [ptr], [blen], self.d_cuts.data_ptr(),
+                                      self.d_count.data_ptr(), self.d_digests.data_ptr(), hs)
+            # ---- device: per-file incremental digests over the fresh bytes [fed, blen)
+            items = []           # (file index, device ptr, length, final)
+            lo_stream, hi_stream = buf_start + fed, buf_start + blen
+            for fi in range(finalized, len(files)):
+                f = files[fi]
+                a, b = max(f.stream_start, lo_stream), min(f.stream_end, hi_stream)
+                n = b - a if b > a else 0
+                is_final = fi < closed
+                if n == 0 and not is_final:
+                    continue
+                items.append((fi, ptr + (a - buf_start) if n else 0, n, is_final))
+            file_digests = None
+            if items:
+                for fi, _, _, _ in items:
+                    if fi not in states:
+                        states[fi] = torch.from_numpy(self._init_state.copy()).to(self.dev)
+                scratch = torch.zeros((len(items), SLOT), dtype=torch.uint8, device=self.dev)
+                self.hasher.update_device([states[fi].data_ptr() for fi, _, _, _ in items],
+                                          [p for _, p, _, _ in items], [n for _, _, n, _ in items],
+                                          [1 if fin else 0 for _, _, _, fin in items],
+                                          scratch.data_ptr(), hs)
+                file_digests = scratch
+            # ---- results back
+            count = int(self.d_count.cpu()[0])
+            if count < 0:
+                raise RuntimeError('cut capacity overflow')
+            ends = self.d_cuts[:count].cpu().numpy().view(np.uint64).astype(np.int64)
+            digs = self.d_digests[:count, :self.digest_size].cpu().numpy()
+            if file_digests is not None:
+                fd = file_digests[:, :self.digest_size].cpu().numpy()
+                for j, (fi, _, _, fin) in enumerate(items):
+                    if fin:
+                        files[fi].digest = fd[j].tobytes()
+                        del states[fi]
+            while finalized < closed and files[finalized].digest is not None:
+                finalized += 1
+            prev = 0
+            for k, e in enumerate(ends.tolist()):
+                d = digs[k].tobytes()
+                idx = table.get(d)
+                if idx is None:
+                    idx = table[d] = len(table)
+                chunks.append(ChunkRecord(counter=len(chunks) + 1, stream_start=buf_start + prev,
+                                          stream_end=buf_start + e, digest=d, table_index=idx,
+                                          contents=hnp[prev:e].tobytes() if self.keep_contents else None))
+                prev = e
+            if final:
+                if prev != blen:
+                    raise RuntimeError(f'final batch left {blen - prev} bytes uncut')
+                break
+            # carry the uncut tail (< max_length bytes) to the front of the buffer
+            tail = blen - prev
+            if tail:
+                hnp[:tail] = hnp[prev:blen].copy()
+            buf_start += prev
+            blen = tail
+            fed = blen
+        return SnapshotStream(files=files, chunks=chunks, chunks_table=table)
+
+
+def snapshot_stream(paths, **kw) -> SnapshotStream:
+    """One-shot helper: DeviceSnapshotProducer(**kw).run(paths)."""
+    return DeviceSnapshotProducer(**kw).run(paths)
+
+
+__all__ = ['DeviceSnapshotProducer', 'SnapshotStream', 'FileRecord', 'ChunkRecord',
+           'tagged_pieces', 'snapshot_stream', 'DEFAULT_BATCH']

@@ -1,0 +1,102 @@
+"""GPU parity of the device snapshot producer (replicat_amd/pipeline.py): replicat's
+_stream_files + _chunk_producer + _chunk_done (repository.py:1374-1505) with chunks, chunk
+digests and per-file digests computed on the device from one upload per batch.
+
+Expected values: chunk lengths from the reference adapter over the reference framing
+(tests/golden/snapshots.json), the oracle's closed form for other sets, and hashlib.blake2b
+(replicat's hash_digest / incremental_hasher, adapters.py:106-114,224-228) for every digest.
+Runs on an MI355X only (-m gpu)."""
+import hashlib
+import os
+import random
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip('torch')
+if not torch.cuda.is_available():  # pragma: no cover - CPU container
+    pytest.skip('needs an MI355X', allow_module_level=True)
+
+import golden_util as G  # noqa: E402
+from test_snapshot import file_sets, write  # noqa: E402
+
+from replicat_amd import snapshot, synth  # noqa: E402
+from replicat_amd.pipeline import DeviceSnapshotProducer  # noqa: E402
+
+SNAPS = {s['name']: s for s in G.load('snapshots.json')}
+
+
+def check_stream(res, files_data, lengths=None):
+    # chunks tile the stream; contents, digests, counters, dedup indices
+    pos, table = 0, {}
+    for k, c in enumerate(res.chunks):
+        assert c.counter == k + 1 and c.stream_start == pos
+        pos = c.stream_end
+        assert c.digest == hashlib.blake2b(c.contents).digest()
+        assert c.table_index == table.setdefault(c.digest, len(table))
+    if lengths is not None:
+        assert [c.stream_end - c.stream_start for c in res.chunks] == lengths
+    # per-file digests and reassembly from the snapshot_files ranges (repository.py:1374-1411)
+    sf = res.snapshot_files()
+    for f in res.files:
+        data = files_data[os.path.basename(f.path)]
+        assert f.digest == hashlib.blake2b(data).digest(), f.path
+        if data:
+            parts = sf[f.path]['chunks']
+            got = b''.join(res.chunks[p['counter'] - 1].contents[p['range'][0]:p['range'][1]]
+                           for p in parts)
+            assert got == data
+            assert sf[f.path]['digest'] == f.digest
+
+
+@pytest.mark.parametrize('name', sorted(SNAPS))
+def test_reference_snapshots(tmp_path, name):
+    s = SNAPS[name]
+    files_data = file_sets()[name]
+    paths = write(tmp_path, files_data)
+    params = None if s['params'] is None else bytes.fromhex(s['params'])
+    res = DeviceSnapshotProducer(min_length=s['min'], max_length=s['max'], params=params,
+                                 batch_bytes=1 << 20).run(paths)
+    check_stream(res, files_data, s['lengths'])
+    assert len(res.files) == len(files_data)
+
+
+@pytest.mark.parametrize('batch', [1, 3 << 20, 64 << 20])
+def test_many_files_many_batches(oracle, tmp_path, batch):
+    """Small params and small batches: files straddle batches, the carried tail, empty files
+    between batches; cuts against the oracle over the whole framed stream."""
+    rnd = random.Random(batch)
+    files_data = {}
+    for i in range(120):
+        n = rnd.choice([0, 1, 2, 3, 5, 127, 128, 129, rnd.randrange(0, 5000),
+                        rnd.randrange(0, 300_000), rnd.randrange(0, 2_000_000)])
+        files_data['f%03d' % i] = rnd.randbytes(n)
+    paths = write(tmp_path, files_data)
+    mn, mx = 2_000, 80_000
+    key = synth.seeded_key(7)
+    res = DeviceSnapshotProducer(min_length=mn, max_length=mx, params=key,
+                                 batch_bytes=batch).run(paths)
+    pieces = list(snapshot.stream_pieces(snapshot.sort_files(paths)))
+    stream = b''.join(pieces)
+    P = len(stream) - len(pieces[-1]) if pieces else 0
+    ends = oracle.chunk_stream(stream, mn, mx, key, P)
+    lengths = [b - a for a, b in zip([0] + ends[:-1], ends)]
+    check_stream(res, files_data, lengths)
+
+
+def test_big_files_default_params(tmp_path):
+    """Files across the 16 MiB piece size with default params (reference fixture)."""
+    files_data = file_sets()['big_files']
+    paths = write(tmp_path, files_data)
+    s = SNAPS['big_files']
+    res = DeviceSnapshotProducer(min_length=s['min'], max_length=s['max'],
+                                 batch_bytes=20 << 20).run(paths)
+    check_stream(res, files_data, s['lengths'])
+
+
+def test_empty_snapshot(tmp_path):
+    paths = write(tmp_path, {'a': b'', 'b': b''})
+    res = DeviceSnapshotProducer(min_length=256, max_length=512).run(paths)
+    assert res.chunks == []
+    assert [f.digest for f in res.files] == [hashlib.blake2b(b'').digest()] * 2
