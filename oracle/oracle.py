@@ -59,6 +59,15 @@ def lib():
         L.oc_blake2b.argtypes = [_p, _u64, ctypes.c_uint32, _p]
         L.oc_blake2b_chunks.restype = ctypes.c_int
         L.oc_blake2b_chunks.argtypes = [_p, _p, _u64, ctypes.c_uint32, _p]
+        _cp, _u32 = ctypes.c_char_p, ctypes.c_uint32
+        L.oc_aes_block.restype = ctypes.c_int
+        L.oc_aes_block.argtypes = [_cp, _u32, _cp, _p]
+        L.oc_gcm_encrypt.restype = ctypes.c_int
+        L.oc_gcm_encrypt.argtypes = [_cp, _u32, _cp, _u64, _cp, _u64, _p]
+        L.oc_gcm_decrypt.restype = ctypes.c_int
+        L.oc_gcm_decrypt.argtypes = [_cp, _u32, _cp, _u64, _cp, _u64, _p]
+        L.oc_gf_mul.restype = None
+        L.oc_gf_mul.argtypes = [_cp, _cp, _p]
         _lib = L
     return _lib
 
@@ -178,3 +187,44 @@ def blake2b_chunks(stream, ends, digest_size=64):
         assert lib().oc_blake2b_chunks(arr.ctypes.data, e.ctypes.data, len(e), digest_size,
                                        out.ctypes.data) == 0
     return out
+
+
+def aes_block(key, block):
+    """oracle/aesgcm_oracle.c: FIPS 197 AES-{128,192,256} of one 16-byte block."""
+    out = ctypes.create_string_buffer(16)
+    if lib().oc_aes_block(bytes(key), len(key), bytes(block), out):
+        raise ValueError('AES key must be 16, 24 or 32 bytes')
+    return out.raw
+
+
+def gcm_encrypt(key, iv, pt):
+    """AESGCM(key).encrypt(iv, pt, None) = C || T (SP 800-38D restated; adapters.py:131-134
+    prepends the nonce)."""
+    pt = bytes(pt)
+    out = ctypes.create_string_buffer(len(pt) + 16)
+    rc = lib().oc_gcm_encrypt(bytes(key), len(key), bytes(iv), len(iv), pt, len(pt), out)
+    if rc:
+        raise ValueError(f'oc_gcm_encrypt failed ({rc})')
+    return out.raw
+
+
+def gcm_decrypt(key, iv, ct_tag):
+    """AESGCM(key).decrypt(iv, C || T, None); ValueError('InvalidTag') when the tag fails."""
+    ct_tag = bytes(ct_tag)
+    if len(ct_tag) < 16:
+        raise ValueError('InvalidTag')
+    n = len(ct_tag) - 16
+    out = ctypes.create_string_buffer(max(n, 1))
+    rc = lib().oc_gcm_decrypt(bytes(key), len(key), bytes(iv), len(iv), ct_tag, n, out)
+    if rc == 3:
+        raise ValueError('InvalidTag')
+    if rc:
+        raise ValueError(f'oc_gcm_decrypt failed ({rc})')
+    return out.raw[:n]
+
+
+def gf_mul(x, y):
+    """The SP 800-38D product of two 16-byte field elements."""
+    out = ctypes.create_string_buffer(16)
+    lib().oc_gf_mul(bytes(x), bytes(y), out)
+    return out.raw
