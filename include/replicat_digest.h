@@ -99,6 +99,18 @@ int rc_blake2b_update_device(rc_hasher *h, uint64_t n, rc_blake2b_state *const *
                              const uint8_t *const *d_ptrs, const uint64_t *lens,
                              const uint8_t *finals, uint8_t *d_out, void *hip_stream);
 
+/* `derive_shared_subkey(digest)` of every chunk rc_blake2b_chunks digested for the same streams
+ * (repository.py:132-137, 1470-1472 -> adapters.py:205-213: hashlib.blake2b(digest,
+ * salt=shared_kdf_params, key=shared_key, digest_size=cipher key bytes)).  For cut slot s the
+ * DEVICE state d_kdf_state -- rc_blake2b_state_init(key_bytes, shared_key, salt=shared_kdf_params);
+ * only read -- absorbs the first msg_len bytes of d_digests + 64 s, and its digest goes to
+ * d_keys + 64 s, where rc_gcm_encrypt_chunks (replicat_cipher.h) takes it.  Counts are read on the
+ * device.  Enqueued on hip_stream. */
+int rc_blake2b_derive_chunks(rc_hasher *h, const rc_chunker *layout, uint64_t n,
+                             const uint64_t *lens, const int64_t *d_counts,
+                             const rc_blake2b_state *d_kdf_state, const uint8_t *d_digests,
+                             uint32_t msg_len, uint8_t *d_keys, void *hip_stream);
+
 /* Kernel timing for bench.py: while enabled, each rc_blake2b_* enqueue records HIP events around
  * its kernels on the launch stream; read returns the summed milliseconds and clears. */
 int rc_blake2b_timing_enable(rc_hasher *h, int enable);

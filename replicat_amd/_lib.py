@@ -18,6 +18,9 @@ RC_ERR_MIN_GT_MAX = 2
 RC_ERR_BAD_KEY = 3
 RC_ERR_DIGEST_SIZE = 4
 RC_ERR_B2_PARAM = 5
+RC_ERR_KEY_SIZE = 6
+RC_ERR_NONCE_SIZE = 7
+RC_ERR_TAG = 8
 RC_ERR_ARGUMENT = 10
 RC_ERR_ALIGN = 11
 RC_ERR_HIP = 12
@@ -26,7 +29,7 @@ RC_ERR_NO_DEVICE = 14
 RC_OPEN = 1
 RC_DIGEST_SLOT = 64
 
-# every symbol include/replicat_chunker.h and include/replicat_digest.h declare:
+# every symbol include/replicat_chunker.h, replicat_digest.h and replicat_cipher.h declare:
 # name -> (restype, argtypes)
 _u64, _i64, _u32, _int, _p = ctypes.c_uint64, ctypes.c_int64, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p
 SIGNATURES = {
@@ -63,6 +66,20 @@ SIGNATURES = {
     'rc_blake2b_update_device': (_int, [_p, _u64, _p, _p, _p, _p, _p, _p]),
     'rc_blake2b_timing_enable': (_int, [_p, _int]),
     'rc_blake2b_timing_read': (_int, [_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_u64)]),
+    'rc_blake2b_derive_chunks': (_int, [_p, _p, _u64, _p, _p, _p, _p, _u32, _p, _p]),
+    # replicat_cipher.h
+    'rc_gcm_create': (_int, [_u32, _u32, _int, ctypes.POINTER(_p)]),
+    'rc_gcm_destroy': (None, [_p]),
+    'rc_gcm_key_bytes': (_u32, [_p]),
+    'rc_gcm_nonce_bytes': (_u32, [_p]),
+    'rc_gcm_encrypt_device': (_int, [_p, _u64, _p, _p, _p, _p, _p, _p]),
+    'rc_gcm_decrypt_device': (_int, [_p, _u64, _p, _p, _p, _p, _p, _p]),
+    'rc_gcm_encrypt_host': (_int, [_p, _u64, _p, _p, _p, _p, _p]),
+    'rc_gcm_decrypt_host': (_int, [_p, _u64, _p, _p, _p, _p, _p]),
+    'rc_gcm_chunks_layout': (_u64, [_p, _p, _u64, _p, _p]),
+    'rc_gcm_encrypt_chunks': (_int, [_p, _p, _u64, _p, _p, _p, _p, _p, _p, _p, _p]),
+    'rc_gcm_timing_enable': (_int, [_p, _int]),
+    'rc_gcm_timing_read': (_int, [_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_u64)]),
 }
 
 
@@ -114,7 +131,7 @@ def check(code):
         return
     msg = last_error()
     if code in (RC_ERR_KEY_LENGTH, RC_ERR_MIN_GT_MAX, RC_ERR_BAD_KEY, RC_ERR_DIGEST_SIZE,
-                RC_ERR_B2_PARAM):
+                RC_ERR_B2_PARAM, RC_ERR_KEY_SIZE, RC_ERR_NONCE_SIZE):
         raise ValueError(msg)
     if code == RC_ERR_NO_DEVICE:
         raise ChunkerUnavailable(msg)

@@ -331,7 +331,65 @@ __global__ __launch_bounds__(kB2Threads) void rc_b2_kernel(const B2Item *__restr
 // value, the byte counter and the last 1..128 message bytes not yet compressed (BLAKE2b may
 // compress a block only once it knows whether the block is the last).  A keyed state starts
 // with the zero-padded key as its pending block (RFC 7693 §3.3), so a keyed or salted hash is
-// the same walk.  Non-final items write the state back; final items write the digest only.
+// the same walk.  Non-final items write the state back; final items write the digest (to `out`)
+// only, so one read-only state may serve many final items.
+__device__ __forceinline__ void b2_update(uint64_t *qb, int q, const LaneCtx &cx,
+                                          rc_blake2b_state *st, gbytes p, uint64_t len, bool final,
+                                          uint8_t *out) {
+    uint8_t *qbb = reinterpret_cast<uint8_t *>(qb);
+    uint64_t h0 = st->h[q], h1 = st->h[q + 4];
+    uint64_t t = st->t;
+    const uint64_t buflen = st->buflen;
+    const uint32_t outlen = st->digest_size;
+    const uint64_t tot = buflen + len;
+    if (!final && tot <= 128) {  // still one pending block: append
+        for (uint64_t j = q; j < len; j += 4) st->buf[buflen + j] = p[j];
+        if (q == 0) st->buflen = tot;
+        return;
+    }
+    if (buflen) {  // pending bytes + the first bytes of p form the next block
+#pragma unroll 4
+        for (int i = 0; i < 32; ++i) {
+            const uint64_t j = 32 * q + i;
+            uint8_t v = 0;
+            if (j < buflen)
+                v = st->buf[j];
+            else if (j - buflen < len)
+                v = p[j - buflen];
+            qbb[j] = v;
+        }
+        if (tot <= 128) {  // final and short: this is the last block
+            compress(h0, h1, cx, t + tot, true);
+            write_digest(out, q, h0, h1, outlen);
+            return;
+        }
+        compress(h0, h1, cx, t + 128, false);
+        t += 128;
+        p += 128 - buflen;
+        len -= 128 - buflen;
+    }
+    const uint64_t nfull = len ? (len - 1) / 128 : 0;
+    gbytes lb = p + 32 * q;
+    const uint32_t sh = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(lb) & 3);
+    gbytes a4 = lb - sh;
+    body_blocks(h0, h1, cx, qb, q, a4, sh, nfull, t);
+    stage_last(qb, q, p, a4, sh, nfull, len);
+    if (final) {
+        compress(h0, h1, cx, t + len, true);
+        write_digest(out, q, h0, h1, outlen);
+    } else {  // keep the last 1..128 bytes pending
+        u32x4 *dst = reinterpret_cast<u32x4 *>(st->buf + 32 * q);
+        dst[0] = *reinterpret_cast<const u32x4 *>(qb + 4 * q);
+        dst[1] = *reinterpret_cast<const u32x4 *>(qb + 4 * q + 2);
+        st->h[q] = h0;
+        st->h[q + 4] = h1;
+        if (q == 0) {
+            st->t = t + 128 * nfull;
+            st->buflen = len - 128 * nfull;
+        }
+    }
+}
+
 __global__ __launch_bounds__(kB2Threads) void rc_b2_update_kernel(const B2UItem *__restrict__ items,
                                                                   uint64_t total,
                                                                   uint8_t *__restrict__ out) {
@@ -339,66 +397,44 @@ __global__ __launch_bounds__(kB2Threads) void rc_b2_update_kernel(const B2UItem 
     const int q = threadIdx.x & 3;
     const int quad = threadIdx.x >> 2;
     uint64_t *qb = blocks + quad * 16;
-    uint8_t *qbb = reinterpret_cast<uint8_t *>(qb);
     const LaneCtx cx = make_ctx(q, qb);
 
     const uint64_t nq = uint64_t(gridDim.x) * (kB2Threads / 4);
     for (uint64_t g = uint64_t(blockIdx.x) * (kB2Threads / 4) + quad; g < total; g += nq) {
         const B2UItem it = items[g];
-        rc_blake2b_state *st = reinterpret_cast<rc_blake2b_state *>(it.state);
-        uint64_t h0 = st->h[q], h1 = st->h[q + 4];
-        uint64_t t = st->t;
-        const uint64_t buflen = st->buflen;
-        const uint32_t outlen = st->digest_size;
-        gbytes p = reinterpret_cast<gbytes>(it.ptr);
-        uint64_t len = it.len;
-        const bool final = it.final != 0;
-        const uint64_t tot = buflen + len;
-        if (!final && tot <= 128) {  // still one pending block: append
-            for (uint64_t j = q; j < len; j += 4) st->buf[buflen + j] = p[j];
-            if (q == 0) st->buflen = tot;
-            continue;
-        }
-        if (buflen) {  // pending bytes + the first bytes of p form the next block
-#pragma unroll 4
-            for (int i = 0; i < 32; ++i) {
-                const uint64_t j = 32 * q + i;
-                uint8_t v = 0;
-                if (j < buflen)
-                    v = st->buf[j];
-                else if (j - buflen < len)
-                    v = p[j - buflen];
-                qbb[j] = v;
-            }
-            if (tot <= 128) {  // final and short: this is the last block
-                compress(h0, h1, cx, t + tot, true);
-                write_digest(out + it.slot * kB2Slot, q, h0, h1, outlen);
-                continue;
-            }
-            compress(h0, h1, cx, t + 128, false);
-            t += 128;
-            p += 128 - buflen;
-            len -= 128 - buflen;
-        }
-        const uint64_t nfull = len ? (len - 1) / 128 : 0;
-        gbytes lb = p + 32 * q;
-        const uint32_t sh = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(lb) & 3);
-        gbytes a4 = lb - sh;
-        body_blocks(h0, h1, cx, qb, q, a4, sh, nfull, t);
-        stage_last(qb, q, p, a4, sh, nfull, len);
-        if (final) {
-            compress(h0, h1, cx, t + len, true);
-            write_digest(out + it.slot * kB2Slot, q, h0, h1, outlen);
-        } else {  // keep the last 1..128 bytes pending
-            u32x4 *dst = reinterpret_cast<u32x4 *>(st->buf + 32 * q);
-            dst[0] = *reinterpret_cast<const u32x4 *>(qb + 4 * q);
-            dst[1] = *reinterpret_cast<const u32x4 *>(qb + 4 * q + 2);
-            st->h[q] = h0;
-            st->h[q + 4] = h1;
-            if (q == 0) {
-                st->t = t + 128 * nfull;
-                st->buflen = len - 128 * nfull;
-            }
+        b2_update(qb, q, cx, reinterpret_cast<rc_blake2b_state *>(it.state),
+                  reinterpret_cast<gbytes>(it.ptr), it.len, it.final != 0, out + it.slot * kB2Slot);
+    }
+}
+
+// Per-chunk subkeys: `derive_shared_subkey(digest)` of every cut slot (repository.py:132-137,
+// 1470-1472; adapters.py:205-213 = hashlib.blake2b(digest, salt=params, key=shared_key,
+// digest_size=key bytes)).  The KDF state (key pending, salt in the parameter block) absorbs the
+// first msg_len bytes of digest slot s and finalises into keys + 64 s.  One quad per chunk; the
+// state is only read.
+struct DeriveLists {
+    const uint64_t *cut_base;
+    const int64_t *counts;
+    uint64_t n, spw;  // streams, streams per workgroup
+};
+
+__global__ __launch_bounds__(kB2Threads) void rc_b2_derive_kernel(DeriveLists c,
+                                                                  rc_blake2b_state *kdf,
+                                                                  uint64_t digests, uint32_t msg_len,
+                                                                  uint8_t *__restrict__ keys) {
+    __shared__ uint64_t blocks[kB2Threads / 4 * 16];
+    const int q = threadIdx.x & 3;
+    const int quad = threadIdx.x >> 2;
+    uint64_t *qb = blocks + quad * 16;
+    const LaneCtx cx = make_ctx(q, qb);
+    const uint64_t s0 = blockIdx.x * c.spw, s1 = s0 + c.spw < c.n ? s0 + c.spw : c.n;
+    for (uint64_t s = s0; s < s1; ++s) {
+        const int64_t cnt = c.counts[s];
+        const uint64_t base = c.cut_base[s];
+        for (int64_t k = quad; k < cnt; k += kB2Threads / 4) {
+            const uint64_t slot = base + uint64_t(k);
+            b2_update(qb, q, cx, kdf, reinterpret_cast<gbytes>(digests + kB2Slot * slot), msg_len,
+                      true, keys + kB2Slot * slot);
         }
     }
 }
@@ -561,4 +597,22 @@ int rc_b2_launch_update(const B2UItem *d_items, uint64_t n, uint8_t *d_out, hipS
     if (!n) return 0;
     rc_b2_update_kernel<<<b2_grid(n), kB2Threads, 0, stream>>>(d_items, n, d_out);
     return b2_status("rc_b2_update_kernel");
+}
+
+int rc_b2_launch_scan(const int64_t *d_counts, uint64_t n, uint64_t *d_chunk_off, hipStream_t stream) {
+    if (!n) return 0;
+    rc_b2_scan_kernel<<<1, 1024, 0, stream>>>(d_counts, n, d_chunk_off);
+    return b2_status("rc_b2_scan_kernel");
+}
+
+int rc_b2_launch_derive(uint64_t n, const uint64_t *d_cut_base, const int64_t *d_counts,
+                        const rc_blake2b_state *d_kdf, const uint8_t *d_digests, uint32_t msg_len,
+                        uint8_t *d_keys, hipStream_t stream) {
+    if (!n) return 0;
+    const DeriveLists c{d_cut_base, d_counts, n, rc_b2_streams_per_group(n)};
+    const unsigned groups = static_cast<unsigned>((n + c.spw - 1) / c.spw);
+    rc_b2_derive_kernel<<<groups, kB2Threads, 0, stream>>>(c, const_cast<rc_blake2b_state *>(d_kdf),
+                                                           reinterpret_cast<uint64_t>(d_digests),
+                                                           msg_len, d_keys);
+    return b2_status("rc_b2_derive_kernel");
 }

@@ -389,6 +389,43 @@ int rc_blake2b_update_device(rc_hasher *h, uint64_t n, rc_blake2b_state *const *
                           static_cast<hipStream_t>(hip_stream));
 }
 
+int rc_blake2b_derive_chunks(rc_hasher *h, const rc_chunker *layout, uint64_t n,
+                             const uint64_t *lens, const int64_t *d_counts,
+                             const rc_blake2b_state *d_kdf_state, const uint8_t *d_digests,
+                             uint32_t msg_len, uint8_t *d_keys, void *hip_stream) {
+    if (!h || !layout) return rc_fail(RC_ERR_ARGUMENT, "null hasher or chunker");
+    if (n == 0) return RC_OK;
+    if (!lens || !d_counts || !d_kdf_state || !d_digests || !d_keys)
+        return rc_fail(RC_ERR_ARGUMENT, "null arrays");
+    if (msg_len > kB2Slot) return rc_fail(RC_ERR_ARGUMENT, "msg_len above the 64-byte digest slot");
+    if (reinterpret_cast<uintptr_t>(d_kdf_state) & 15)
+        return rc_fail(RC_ERR_ARGUMENT, "KDF state not 16-byte aligned");
+    std::vector<uint64_t> caps(n);
+    rc_cut_capacity(layout, n, lens, caps.data());
+    std::lock_guard<std::mutex> lock(h->mu);
+    Guard g(h->device);
+    const hipStream_t st = static_cast<hipStream_t>(hip_stream);
+    Workspace *w = nullptr;
+    if (int rc = acquire(h, w)) return rc;
+    const size_t bytes = n * sizeof(uint64_t);
+    if (int rc = w->h_stage.ensure(bytes)) return rc;
+    if (int rc = w->d_stage.ensure(bytes)) return rc;
+    uint64_t *u = static_cast<uint64_t *>(w->h_stage.p);
+    uint64_t acc = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        u[i] = acc;
+        acc += caps[i];
+    }
+    RC_HIP_TRY(hipMemcpyAsync(w->d_stage.p, u, bytes, hipMemcpyHostToDevice, st));
+    std::array<hipEvent_t, 2> ev{};
+    if (int rc = timing_begin(h, st, ev)) return rc;
+    if (rc_b2_launch_derive(n, static_cast<const uint64_t *>(w->d_stage.p), d_counts, d_kdf_state,
+                            d_digests, msg_len, d_keys, st))
+        return rc_fail(RC_ERR_HIP, "%s", rc_b2_launch_error());
+    if (int rc = timing_end(h, st, ev)) return rc;
+    return finish(h, *w, st);
+}
+
 int rc_blake2b_timing_enable(rc_hasher *h, int enable) {
     if (!h) return rc_fail(RC_ERR_ARGUMENT, "null hasher");
     h->timing = enable != 0;

@@ -46,3 +46,12 @@ int rc_b2_launch_chunks(uint64_t n, const uint64_t *d_ptrs, const uint64_t *d_cu
                         const uint64_t *d_cuts, const int64_t *d_counts, uint64_t *d_chunk_off,
                         uint32_t *d_hist, B2Item *d_items, uint64_t items_cap, uint32_t outlen,
                         uint8_t *d_out, hipStream_t stream);
+
+// Exclusive prefix of the per-stream chunk counts into d_chunk_off[0..n] (the total at [n]).
+int rc_b2_launch_scan(const int64_t *d_counts, uint64_t n, uint64_t *d_chunk_off, hipStream_t stream);
+
+// derive_shared_subkey of every cut slot (rc_b2_derive_kernel): the read-only KDF state absorbs
+// msg_len bytes of digest slot s and finalises into d_keys + 64 s.  d_cut_base has n entries.
+int rc_b2_launch_derive(uint64_t n, const uint64_t *d_cut_base, const int64_t *d_counts,
+                        const rc_blake2b_state *d_kdf, const uint8_t *d_digests, uint32_t msg_len,
+                        uint8_t *d_keys, hipStream_t stream);

@@ -21,7 +21,8 @@ and the incremental / keyed half of the adapter over device-resident states
 * ``update_device(states, ptrs, lens, finals, out)`` -- many HashlibIncrementalHasher.feed /
   .digest steps (adapters.py:106-114) in one launch: per-file digests (repository.py:1433-1446),
   the shared-subkey KDF ``derive`` (adapters.py:203-211) and ``mac`` (:217-221);
-* ``DeviceIncrementalHasher`` -- ``incremental_hasher()`` (adapters.py:227-228) itself.
+* ``DeviceIncrementalHasher`` -- ``incremental_hasher()`` (adapters.py:227-228) itself;
+* ``derive_chunks(...)`` -- the subkey of every chunk digest left in HBM (repository.py:1470-1472).
 
 There is no CPU fallback: without the HIP library every call raises.
 """
@@ -132,6 +133,17 @@ class GpuBlake2b:
         check(lib().rc_blake2b_update_device(self._h, len(lens), states.ctypes.data,
                                              ptrs.ctypes.data, lens.ctypes.data,
                                              fin.ctypes.data, out_ptr or None, stream or None))
+
+    def derive_chunks(self, chunker, lens, counts_ptr, kdf_state_ptr, digests_ptr, keys_ptr,
+                      stream=0):
+        """Enqueue ``derive_shared_subkey(digest)`` of every chunk digest ``digest_chunks`` left
+        in HBM (repository.py:132-137, 1470-1472; adapters.py:205-213): the device state at
+        kdf_state_ptr -- ``state_init(key_bytes, key=shared_key, salt=shared_kdf_params)``, only
+        read -- absorbs the digest of cut slot s and its digest lands at keys + 64 s."""
+        lens = _ptr_array(lens)
+        check(lib().rc_blake2b_derive_chunks(self._h, chunker._h, len(lens), lens.ctypes.data,
+                                             counts_ptr, kdf_state_ptr, digests_ptr,
+                                             self.digest_size, keys_ptr, stream or None))
 
     # ---------------------------------------------------------------------- profiling
 

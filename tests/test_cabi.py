@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def header_symbols():
     text = ''.join(open(os.path.join(ROOT, 'include', h)).read()
-                   for h in ('replicat_chunker.h', 'replicat_digest.h'))
+                   for h in ('replicat_chunker.h', 'replicat_digest.h', 'replicat_cipher.h'))
     return sorted(set(re.findall(r'^\w[\w\s\*]*?\b(rc_\w+)\s*\(', text, re.M)))
 
 
