@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <array>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -45,21 +46,34 @@ struct DevBuf {
     }
 };
 
+// Staging memory: pinned when the runtime grants it, else pageable (copies from pageable memory
+// are synchronous, which every user of these buffers tolerates).
 struct HostBuf {
     void *p = nullptr;
     size_t n = 0;
+    bool pinned = false;
     int ensure(size_t bytes) {
         if (bytes <= n) return 0;
-        if (p) RC_HIP_TRY(hipHostFree(p));
-        p = nullptr;
-        n = 0;
+        release();
         const size_t want = std::max<size_t>(bytes, 4096);
-        RC_HIP_TRY(hipHostMalloc(&p, want, hipHostMallocDefault));
+        if (hipHostMalloc(&p, want, hipHostMallocDefault) == hipSuccess) {
+            pinned = true;
+        } else {
+            (void)hipGetLastError();  // clear the failed allocation's status
+            p = std::malloc(want);
+            pinned = false;
+            if (!p) return rc_fail(RC_ERR_HIP, "host staging: %zu bytes unavailable", want);
+        }
         n = want;
         return 0;
     }
     void release() {
-        if (p) (void)hipHostFree(p);
+        if (p) {
+            if (pinned)
+                (void)hipHostFree(p);
+            else
+                std::free(p);
+        }
         p = nullptr;
         n = 0;
     }

@@ -1,27 +1,29 @@
-"""replicat's snapshot chunk producer on the device (SURVEY.md §8 f, ranks 1-3 together).
+"""replicat's snapshot chunk producer on the device (SURVEY.md §8 f, ranks 1-4 together).
 
 What it replaces, in /root/reference/replicat/repository.py:
 
 * ``_stream_files`` (:1413-1452): files sorted by (size, path), read in 16 MiB pieces, zero
   padding to 4 bytes between files, and a ``blake2b`` incremental hasher per file (:1433-1446);
 * ``_chunk_producer`` (:1454-1505): ``chunkify`` over that ONE stream, ``hash_digest`` of every
-  chunk (:1462), the digest -> table-index dedup map (:1464-1468), the chunk counter and
-  stream offsets (:1457-1459, :1477-1485);
+  chunk (:1462), the digest -> table-index dedup map (:1464-1468), for an encrypted repository
+  ``encrypt(chunk, derive_shared_subkey(digest))`` (:1470-1473), the chunk counter and stream
+  offsets (:1457-1459, :1477-1485);
 * ``_chunk_done``'s file -> chunk-range map (:1374-1411).
 
 The stream is gathered into host batches (``batch_bytes``, pinned) exactly as the batching shim
 does (replicat_amd/adapters.py): every batch but the last is chunked as an OPEN prefix (the
 reference's non-final ``next_cut`` calls), the last with its real framing, and the uncut tail
-is carried into the next batch.  Each batch is uploaded ONCE and three things run on the bytes
-in HBM: the cut chain (rc_chunk_device), the chunk digests (rc_blake2b_chunks) and the per-file
-incremental digests (rc_blake2b_update_device: each file's bytes are fed once, in the batch
-that first holds them; a file's state lives in HBM across batches).  Only cut offsets and
-digests come back -- and the chunk bytes, which replicat uploads, are sliced from the host
-batch.
+is carried into the next batch.  Each batch is uploaded ONCE and everything runs on the bytes in
+HBM: the cut chain (rc_chunk_device), the chunk digests (rc_blake2b_chunks), the per-file
+incremental digests (rc_blake2b_update_device: each file's bytes are fed once, in the batch that
+first holds them; a file's state lives in HBM across batches) and, with ``encryption``, every
+chunk's subkey (rc_blake2b_derive_chunks) and its AES-GCM encryption (rc_gcm_encrypt_chunks).
+Only cut offsets, digests and -- what replicat uploads -- the chunk contents come back: sliced
+from the host batch, or the device's nonce || C || T when encrypted.
 
 The dedup table and the chunk -> file range map are host bookkeeping on a few integers per
-chunk, as in the reference.  There is no CPU fallback: every digest and cut comes from the HIP
-library.
+chunk, as in the reference.  There is no CPU fallback: every cut, digest and ciphertext comes
+from the HIP library.
 """
 import bisect
 import os
@@ -48,13 +50,26 @@ class FileRecord:
 
 @dataclass
 class ChunkRecord:
-    """repository.py:1477-1485 (_SnapshotChunk) without the upload location."""
+    """repository.py:1477-1485 (_SnapshotChunk) without the upload location.  ``contents`` is
+    what replicat uploads: the chunk bytes, or nonce || C || T for an encrypted repository."""
     counter: int
     stream_start: int
     stream_end: int
     digest: bytes
     table_index: int
     contents: Optional[bytes] = field(default=None, repr=False)
+
+
+@dataclass
+class ChunkEncryption:
+    """What an encrypted repository's snapshot loop needs to encrypt chunks
+    (repository.py:1470-1473): KeyProps.params['shared_key'] and ['shared_kdf_params']
+    (repository.py:132-137) and the cipher's aes_gcm settings (adapters.py:151-158).  The shared
+    KDF is blake2b(length=key_bits // 8) (repository.py:623-627)."""
+    shared_key: bytes
+    shared_kdf_params: bytes
+    key_bits: int = 256
+    nonce_bits: int = 96
 
 
 @dataclass
@@ -107,11 +122,13 @@ def tagged_pieces(paths: Sequence[str], files: List[FileRecord], read=None
 
 
 class DeviceSnapshotProducer:
-    """Chunks, chunk digests and file digests of a snapshot's stream on one HIP device."""
+    """Chunks, chunk digests, file digests and (optionally) encrypted chunks of a snapshot's
+    stream on one HIP device."""
 
     def __init__(self, *, min_length: int = MIN_LENGTH, max_length: int = MAX_LENGTH,
                  params: Optional[bytes] = None, digest_size: int = 64,
-                 batch_bytes: int = DEFAULT_BATCH, device=None, keep_contents: bool = True):
+                 batch_bytes: int = DEFAULT_BATCH, device=None, keep_contents: bool = True,
+                 encryption: Optional[ChunkEncryption] = None):
         import torch
         if device is None:
             device = _current_device()
@@ -136,6 +153,20 @@ class DeviceSnapshotProducer:
         self.d_count = torch.zeros(1, dtype=torch.int64, device=self.dev)
         self.d_digests = torch.zeros((max(total, 1), SLOT), dtype=torch.uint8, device=self.dev)
         self._init_state = np.frombuffer(state_init(digest_size), dtype=np.uint8)
+        self.encryption = encryption
+        if encryption is not None:
+            from .cipher import GpuAesGcm
+            self.cipher = GpuAesGcm(key_bits=encryption.key_bits, nonce_bits=encryption.nonce_bits,
+                                    device=self.device)
+            kdf = state_init(self.cipher.key_bytes, key=encryption.shared_key,
+                             salt=encryption.shared_kdf_params)
+            self.d_kdf = torch.from_numpy(np.frombuffer(kdf, dtype=np.uint8).copy()).to(self.dev)
+            self.d_keys = torch.zeros((max(total, 1), SLOT), dtype=torch.uint8, device=self.dev)
+            nb = self.cipher.nonce_bytes
+            self.h_nonces = torch.empty(max(total, 1) * nb, dtype=torch.uint8, pin_memory=True)
+            self.d_nonces = torch.empty(max(total, 1) * nb, dtype=torch.uint8, device=self.dev)
+            out_total, _ = self.cipher.chunks_layout(self.chunker, [self.capacity])
+            self.d_enc = torch.empty(max(out_total, 1), dtype=torch.uint8, device=self.dev)
 
     # ------------------------------------------------------------------------------ run
 
@@ -172,6 +203,18 @@ class DeviceSnapshotProducer:
                                       self.d_count.data_ptr(), hs, open_=not final)
             self.hasher.digest_chunks(self.chunker, [ptr], [blen], self.d_cuts.data_ptr(),
                                       self.d_count.data_ptr(), self.d_digests.data_ptr(), hs)
+            if self.encryption is not None:
+                # derive_shared_subkey(digest) and encrypt, per chunk, still in HBM; one
+                # os.urandom nonce per chunk as the adapter draws them (adapters.py:133)
+                self.hasher.derive_chunks(self.chunker, [blen], self.d_count.data_ptr(),
+                                          self.d_kdf.data_ptr(), self.d_digests.data_ptr(),
+                                          self.d_keys.data_ptr(), hs)
+                self.h_nonces.numpy()[:] = np.frombuffer(os.urandom(self.h_nonces.numel()),
+                                                         dtype=np.uint8)
+                self.d_nonces.copy_(self.h_nonces, non_blocking=True)
+                self.cipher.encrypt_chunks(self.chunker, [ptr], [blen], self.d_cuts.data_ptr(),
+                                           self.d_count.data_ptr(), self.d_keys.data_ptr(),
+                                           self.d_nonces.data_ptr(), self.d_enc.data_ptr(), hs)
             # ---- device: per-file incremental digests over the fresh bytes [fed, blen)
             items = []           # (file index, device ptr, length, final)
             lo_stream, hi_stream = buf_start + fed, buf_start + blen
@@ -200,6 +243,11 @@ class DeviceSnapshotProducer:
                 raise RuntimeError('cut capacity overflow')
             ends = self.d_cuts[:count].cpu().numpy().view(np.uint64).astype(np.int64)
             digs = self.d_digests[:count, :self.digest_size].cpu().numpy()
+            enc = None
+            if self.encryption is not None:
+                over = self.cipher.nonce_bytes + 16
+                n_out = (int(ends[-1]) if count else 0) + count * over
+                enc = self.d_enc[:n_out].cpu().numpy()
             if file_digests is not None:
                 fd = file_digests[:, :self.digest_size].cpu().numpy()
                 for j, (fi, _, _, fin) in enumerate(items):
@@ -214,9 +262,14 @@ class DeviceSnapshotProducer:
                 idx = table.get(d)
                 if idx is None:
                     idx = table[d] = len(table)
+                if enc is not None:  # nonce || C || T of chunk k at prev + k (nonce_bytes + 16)
+                    o = prev + k * over
+                    contents = enc[o:o + (e - prev) + over].tobytes()
+                else:
+                    contents = hnp[prev:e].tobytes() if self.keep_contents else None
                 chunks.append(ChunkRecord(counter=len(chunks) + 1, stream_start=buf_start + prev,
                                           stream_end=buf_start + e, digest=d, table_index=idx,
-                                          contents=hnp[prev:e].tobytes() if self.keep_contents else None))
+                                          contents=contents))
                 prev = e
             if final:
                 if prev != blen:
@@ -237,5 +290,5 @@ def snapshot_stream(paths, **kw) -> SnapshotStream:
     return DeviceSnapshotProducer(**kw).run(paths)
 
 
-__all__ = ['DeviceSnapshotProducer', 'SnapshotStream', 'FileRecord', 'ChunkRecord',
+__all__ = ['DeviceSnapshotProducer', 'SnapshotStream', 'FileRecord', 'ChunkRecord', 'ChunkEncryption',
            'tagged_pieces', 'snapshot_stream', 'DEFAULT_BATCH']

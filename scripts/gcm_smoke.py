@@ -2,6 +2,7 @@
 import sys
 
 sys.path.insert(0, '.')
+import torch  # noqa: E402,F401  (the HIP runtime as the tests see it)
 from oracle import oracle as o  # noqa: E402
 from replicat_amd.cipher import GpuAesGcm  # noqa: E402
 
