@@ -129,12 +129,11 @@ class GpuAesGcm:
             ks = [np.frombuffer(keys[i], dtype=np.uint8) for i in idx]
             ns = [np.frombuffer(nonces[i], dtype=np.uint8) for i in idx]
             outs = [np.empty(self._nonce_bytes + a.size + TAG_BYTES, dtype=np.uint8) for a in ins]
-            check(lib().rc_gcm_encrypt_host(
-                h, len(idx), _ptr_array([a.ctypes.data if a.size else 0 for a in ins]).ctypes.data,
-                _ptr_array([a.size for a in ins]).ctypes.data,
-                _ptr_array([a.ctypes.data for a in ks]).ctypes.data,
-                _ptr_array([a.ctypes.data for a in ns]).ctypes.data,
-                _ptr_array([a.ctypes.data for a in outs]).ctypes.data))
+            # the pointer arrays stay referenced for the whole call
+            arrs = (_ptr_array([a.ctypes.data if a.size else 0 for a in ins]),
+                    _ptr_array([a.size for a in ins]), _ptr_array([a.ctypes.data for a in ks]),
+                    _ptr_array([a.ctypes.data for a in ns]), _ptr_array([a.ctypes.data for a in outs]))
+            check(lib().rc_gcm_encrypt_host(h, len(idx), *[a.ctypes.data for a in arrs]))
             for i, o in zip(idx, outs):
                 out[i] = o.tobytes()
         return out
@@ -155,11 +154,11 @@ class GpuAesGcm:
             ks = [np.frombuffer(keys[i], dtype=np.uint8) for i in idx]
             outs = [np.empty(max(a.size - over, 1), dtype=np.uint8) for a in ins]
             ok = np.zeros(len(idx), dtype=np.uint8)
-            rc = lib().rc_gcm_decrypt_host(
-                h, len(idx), _ptr_array([a.ctypes.data if a.size else 0 for a in ins]).ctypes.data,
-                _ptr_array([a.size for a in ins]).ctypes.data,
-                _ptr_array([a.ctypes.data for a in ks]).ctypes.data,
-                _ptr_array([a.ctypes.data for a in outs]).ctypes.data, ok.ctypes.data)
+            arrs = (_ptr_array([a.ctypes.data if a.size else 0 for a in ins]),
+                    _ptr_array([a.size for a in ins]), _ptr_array([a.ctypes.data for a in ks]),
+                    _ptr_array([a.ctypes.data for a in outs]))
+            rc = lib().rc_gcm_decrypt_host(h, len(idx), *[a.ctypes.data for a in arrs],
+                                           ok.ctypes.data)
             if rc not in (0, RC_ERR_TAG):
                 check(rc)
             for j, i in enumerate(idx):
@@ -172,19 +171,19 @@ class GpuAesGcm:
 
     def encrypt_device(self, in_ptrs, lens, key_ptrs, nonce_ptrs, out_ptrs, stream=0):
         """Enqueue encrypt of device buffers: out_ptrs[i] receives nonce || C || T."""
-        lens = _ptr_array(lens)
-        check(lib().rc_gcm_encrypt_device(self.handle(), len(lens), _ptr_array(in_ptrs).ctypes.data,
-                                          lens.ctypes.data, _ptr_array(key_ptrs).ctypes.data,
-                                          _ptr_array(nonce_ptrs).ctypes.data,
-                                          _ptr_array(out_ptrs).ctypes.data, stream or None))
+        ins, lens, ks, ns, outs = (_ptr_array(v) for v in (in_ptrs, lens, key_ptrs, nonce_ptrs,
+                                                           out_ptrs))
+        check(lib().rc_gcm_encrypt_device(self.handle(), len(lens), ins.ctypes.data,
+                                          lens.ctypes.data, ks.ctypes.data, ns.ctypes.data,
+                                          outs.ctypes.data, stream or None))
 
     def decrypt_device(self, in_ptrs, lens, key_ptrs, out_ptrs, ok_ptr, stream=0):
         """Enqueue decrypt of device blobs nonce || C || T (lens: whole blobs); ok_ptr receives
         one byte per blob, 1 when its tag verifies."""
-        lens = _ptr_array(lens)
-        check(lib().rc_gcm_decrypt_device(self.handle(), len(lens), _ptr_array(in_ptrs).ctypes.data,
-                                          lens.ctypes.data, _ptr_array(key_ptrs).ctypes.data,
-                                          _ptr_array(out_ptrs).ctypes.data, ok_ptr, stream or None))
+        ins, lens, ks, outs = (_ptr_array(v) for v in (in_ptrs, lens, key_ptrs, out_ptrs))
+        check(lib().rc_gcm_decrypt_device(self.handle(), len(lens), ins.ctypes.data,
+                                          lens.ctypes.data, ks.ctypes.data, outs.ctypes.data,
+                                          ok_ptr, stream or None))
 
     def chunks_layout(self, chunker, lens):
         """(total bytes, per-stream offsets) of encrypt_chunks' output buffer: chunk k of stream i
