@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <array>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -23,6 +24,20 @@ static_assert(sizeof(GcmItem) == 48, "GcmItem is a 48-byte device record");
 
 namespace {
 
+// RC_GCM_DEBUG=1: every host step of a call is stamped on stderr (hang diagnosis)
+bool debug_on() {
+    static const bool on = std::getenv("RC_GCM_DEBUG") != nullptr;
+    return on;
+}
+#define GCM_DBG(...)                                      \
+    do {                                                  \
+        if (debug_on()) {                                 \
+            std::fprintf(stderr, "rc_gcm: " __VA_ARGS__); \
+            std::fputc('\n', stderr);                     \
+            std::fflush(stderr);                          \
+        }                                                 \
+    } while (0)
+
 struct DevBuf {
     void *p = nullptr;
     size_t n = 0;
@@ -35,6 +50,7 @@ struct DevBuf {
             n = 0;
         }
         const size_t want = (std::max<size_t>(bytes, 4096) + 4095) & ~size_t(4095);
+        GCM_DBG("hipMalloc %zu", want);
         RC_HIP_TRY(hipMalloc(&p, want));
         n = want;
         return 0;
@@ -56,9 +72,11 @@ struct HostBuf {
         if (bytes <= n) return 0;
         release();
         const size_t want = std::max<size_t>(bytes, 4096);
+        GCM_DBG("hipHostMalloc %zu", want);
         if (hipHostMalloc(&p, want, hipHostMallocDefault) == hipSuccess) {
             pinned = true;
         } else {
+            GCM_DBG("hipHostMalloc refused: pageable staging");
             (void)hipGetLastError();  // clear the failed allocation's status
             p = std::malloc(want);
             pinned = false;
@@ -160,7 +178,7 @@ struct rc_gcm {
     std::mutex mu;
     DevBuf d_consts;  // te0 | sq
     struct Workspace {
-        HostBuf h_stage;  // [work counter 16 B] [host-built staging]
+        HostBuf h_stage;  // [header 16 B] [host-built staging]
         DevBuf d_stage;   // its device copy (+ device-built lists)
         hipEvent_t done = nullptr;
         bool pending = false;
@@ -182,6 +200,7 @@ using Workspace = rc_gcm::Workspace;
 int acquire(rc_gcm *g, Workspace *&out) {
     Workspace &w = g->ws[g->next_ws++ & 1];
     if (w.pending) {  // its previous call must have consumed the staging
+        GCM_DBG("wait for workspace %u", (g->next_ws - 1) & 1);
         RC_HIP_TRY(hipEventSynchronize(w.done));
         w.pending = false;
     }
@@ -236,18 +255,18 @@ int enqueue_items(rc_gcm *g, bool dec, std::vector<GcmItem> &items, uint8_t *d_o
     if (int rc = w->h_stage.ensure(bytes)) return rc;
     if (int rc = w->d_stage.ensure(bytes)) return rc;
     uint8_t *h = static_cast<uint8_t *>(w->h_stage.p);
-    std::memset(h, 0, 16);  // the work counter
+    std::memset(h, 0, 16);  // header (reserved)
     std::memcpy(h + 16, items.data(), n * sizeof(GcmItem));
     RC_HIP_TRY(hipMemcpyAsync(w->d_stage.p, h, bytes, hipMemcpyHostToDevice, st));
     uint8_t *d = static_cast<uint8_t *>(w->d_stage.p);
     GcmArgs a = base_args(g);
     a.items = reinterpret_cast<const GcmItem *>(d + 16);
-    a.n = n;
-    a.next = reinterpret_cast<unsigned long long *>(d);
     a.ok = d_ok;
     std::array<hipEvent_t, 2> ev{};
     if (int rc = timing_begin(g, st, ev)) return rc;
-    const unsigned groups = static_cast<unsigned>(std::min<uint64_t>(kGcmMaxGroups, n));
+    if (n > 0x7FFFFFFFull) return rc_fail(RC_ERR_ARGUMENT, "%llu messages in one call", (unsigned long long)n);
+    const unsigned groups = static_cast<unsigned>(n);
+    GCM_DBG("launch %s n=%llu groups=%u", dec ? "decrypt" : "encrypt", (unsigned long long)n, groups);
     if (rc_gcm_launch(g->key_bytes, dec, a, groups, st))
         return rc_fail(RC_ERR_HIP, "%s", rc_gcm_launch_error());
     if (int rc = timing_end(g, st, ev)) return rc;
@@ -395,6 +414,7 @@ int rc_gcm_encrypt_host(rc_gcm *g, uint64_t n, const uint8_t *const *in, const u
         std::memcpy(hi + key_off + 64 * i, keys[i], kb);
         std::memcpy(hi + nonce_off + 128 * i, nonces[i], nb);
     }
+    GCM_DBG("encrypt_host: upload %llu bytes", (unsigned long long)in_total);
     RC_HIP_TRY(hipMemcpyAsync(g->d_in.p, hi, in_total, hipMemcpyHostToDevice, nullptr));
     const uint64_t D = addr(g->d_in.p), O = addr(g->d_out.p);
     std::vector<GcmItem> items(n);
@@ -402,8 +422,11 @@ int rc_gcm_encrypt_host(rc_gcm *g, uint64_t n, const uint8_t *const *in, const u
         items[i] = GcmItem{D + in_off[i], lens[i], O + out_off[i], D + key_off + 64 * i,
                            D + nonce_off + 128 * i, i};
     if (int rc = enqueue_items(g, false, items, nullptr, nullptr)) return rc;
+    GCM_DBG("encrypt_host: download %llu bytes", (unsigned long long)b);
     RC_HIP_TRY(hipMemcpyAsync(ho, g->d_out.p, b, hipMemcpyDeviceToHost, nullptr));
+    GCM_DBG("encrypt_host: synchronize");
     RC_HIP_TRY(hipStreamSynchronize(nullptr));
+    GCM_DBG("encrypt_host: done");
     for (uint64_t i = 0; i < n; ++i) std::memcpy(out[i], ho + out_off[i], nb + lens[i] + 16);
     return RC_OK;
 }
@@ -492,7 +515,7 @@ int rc_gcm_encrypt_chunks(rc_gcm *g, const rc_chunker *layout, uint64_t n,
     const hipStream_t st = static_cast<hipStream_t>(hip_stream);
     Workspace *w = nullptr;
     if (int rc = acquire(g, w)) return rc;
-    // staging: [counter 16 B] ptrs[n] cut_base[n] out_base[n] | device only: chunk_off[n + 1], items
+    // staging: [header 16 B] ptrs[n] cut_base[n] out_base[n] | device only: chunk_off[n + 1], items
     const size_t up = 16 + 3 * n * sizeof(uint64_t);
     const size_t items_off = up16(up + (n + 1) * sizeof(uint64_t));
     if (int rc = w->h_stage.ensure(up)) return rc;
@@ -532,8 +555,9 @@ int rc_gcm_encrypt_chunks(rc_gcm *g, const rc_chunker *layout, uint64_t n,
     GcmArgs a = base_args(g);
     a.items = items;
     a.d_total = chunk_off + n;
-    a.next = reinterpret_cast<unsigned long long *>(d);
-    const unsigned groups = static_cast<unsigned>(std::min<uint64_t>(kGcmMaxGroups, std::max<uint64_t>(total_cap, 1)));
+    if (total_cap > 0x7FFFFFFFull)
+        return rc_fail(RC_ERR_ARGUMENT, "%llu chunk slots in one call", (unsigned long long)total_cap);
+    const unsigned groups = static_cast<unsigned>(std::max<uint64_t>(total_cap, 1));
     if (rc_gcm_launch(g->key_bytes, false, a, groups, st))
         return rc_fail(RC_ERR_HIP, "%s", rc_gcm_launch_error());
     if (int rc = timing_end(g, st, ev)) return rc;

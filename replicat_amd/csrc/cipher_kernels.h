@@ -15,21 +15,19 @@ struct GcmItem {
 
 struct GcmArgs {
     const GcmItem *items;
-    const uint64_t *d_total;   // item count on the device (chunk path), or nullptr: n
-    uint64_t n;
-    unsigned long long *next;  // work counter, zero at launch
+    const uint64_t *d_total;   // item count on the device (chunk path; the grid covers its bound)
     const uint32_t *te0;       // AES T0 table (256 words)
     const uint32_t *sq;        // GF(2^128) squaring nibble table (512 x 16 bytes)
     uint8_t *ok;               // decrypt verdicts
     uint32_t nonce_bytes;
 };
 
-constexpr int kGcmThreads = 1024;        // 16 waves: one workgroup per CU (128 KiB of LDS)
-constexpr unsigned kGcmMaxGroups = 256;  // one per CU
+constexpr int kGcmThreads = 1024;  // 16 waves: one workgroup per CU (128 KiB of LDS)
 
 const char *rc_gcm_launch_error(void);
 
-// AES-GCM over a work list (key_bytes 16 / 24 / 32).
+// AES-GCM over a work list (key_bytes 16 / 24 / 32): workgroup i takes item i; groups = the item
+// count (or, with d_total, its bound).
 int rc_gcm_launch(uint32_t key_bytes, bool decrypt, const GcmArgs &args, unsigned groups,
                   hipStream_t stream);
 

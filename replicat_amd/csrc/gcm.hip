@@ -9,7 +9,7 @@
 //
 // Shape of the work.  CTR mode is parallel over 16-byte blocks; GHASH is the polynomial
 // S = (sum_i C_i H^(m-i) + L) H over the ciphertext blocks C_0..C_(m-1) and the length block L.
-// One workgroup (1024 threads) takes one chunk at a time: thread t owns blocks t, t+1024, .. (each
+// One workgroup (1024 threads) per chunk: thread t owns blocks t, t+1024, .. (each
 // row of 1024 blocks is one coalesced 16 KiB read and write) and folds its blocks by Horner with
 // M = H^1024.  The chunk is virtually left-padded with zero blocks to a whole number of rows
 // (leading zeros do not change a GHASH that starts at 0), so all 1024 chains end in the last row
@@ -36,6 +36,21 @@
 
 #include "cipher_kernels.h"
 
+#ifdef RC_GCM_TRACE  // diagnostic build (scripts/gcm_diag.cpp): progress word of workgroup 0
+__device__ unsigned long long g_gcm_trace[4];
+#define GCM_MARK(code, val)                                                                      \
+    do {                                                                                         \
+        if (blockIdx.x == 0 && threadIdx.x == 0) {                                               \
+            __hip_atomic_store(&g_gcm_trace[0], (unsigned long long)(code), __ATOMIC_RELAXED,    \
+                               __HIP_MEMORY_SCOPE_SYSTEM);                                       \
+            __hip_atomic_store(&g_gcm_trace[1], (unsigned long long)(val), __ATOMIC_RELAXED,     \
+                               __HIP_MEMORY_SCOPE_SYSTEM);                                       \
+        }                                                                                        \
+    } while (0)
+#else
+#define GCM_MARK(code, val) do { } while (0)
+#endif
+
 namespace {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -57,7 +72,6 @@ constexpr uint32_t kH32 = kMisc + 272;
 constexpr uint32_t kHM = kMisc + 288;
 constexpr uint32_t kJ0 = kMisc + 304;
 constexpr uint32_t kEJ0 = kMisc + 320;
-constexpr uint32_t kIdx = kMisc + 336;
 constexpr uint32_t kP = kMisc + 512;  // 32 partial sums
 constexpr uint32_t kAes = 65536;      // 256 rows x 256 B
 constexpr uint32_t kLds = 131072;
@@ -73,12 +87,6 @@ __device__ __forceinline__ T &lds(uint32_t off) {
 __device__ __forceinline__ uint32_t rotl8(uint32_t x) { return (x << 8) | (x >> 24); }
 __device__ __forceinline__ uint32_t rot16(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 16); }
 __device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
-
-__device__ __forceinline__ uint64_t uniform64(uint64_t x) {
-    const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(x));
-    const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(x >> 32));
-    return (uint64_t(hi) << 32) | lo;
-}
 
 // ------------------------------------------------------------------------------ AES
 
@@ -247,8 +255,13 @@ template <int NR, bool DEC>
 __global__ __launch_bounds__(kGcmThreads) void rc_gcm_kernel(GcmArgs a) {
     constexpr int NW = 4 * (NR + 1);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // one workgroup per message, straight-line (no work-queue loop: barriers inside a loop whose
+    // exit the compiler could not prove uniform were structurized into a hang)
+    const uint64_t idx = blockIdx.x;
+    if (a.d_total && idx >= *a.d_total) return;
+    GCM_MARK(2, idx);
 
-    // constant tables, once per workgroup
+    // constant tables
     for (int i = tid; i < 256 * 64; i += kGcmThreads) {
         const int e = i >> 6, c = i & 63;
         const uint32_t t0 = a.te0[e];
@@ -257,20 +270,16 @@ __global__ __launch_bounds__(kGcmThreads) void rc_gcm_kernel(GcmArgs a) {
     for (int i = tid; i < 512; i += kGcmThreads)
         lds<u32x4>(kSq + i * 16) = reinterpret_cast<const u32x4 *>(a.sq)[i];
     const uint32_t lo0 = 0x10000u | (uint32_t(lane & 31) << 2), lo1 = lo0 | 128u;
-    const uint64_t total = a.d_total ? uniform64(*a.d_total) : a.n;
     const uint32_t nbytes = a.nonce_bytes;
-
-    for (;;) {
-        if (tid == 0) lds<uint64_t>(kIdx) = atomicAdd(a.next, 1ull);
-        __syncthreads();
-        const uint64_t idx = uniform64(lds<uint64_t>(kIdx));
-        if (idx >= total) break;
+    {
         const GcmItem it = a.items[idx];
         gcbytes nonce = reinterpret_cast<gcbytes>(DEC ? it.in : it.nonce);
 
         // ---- A: key schedule (one lane)
+        __syncthreads();  // the tables
         if (tid == 0) expand_key<NR>(reinterpret_cast<gcbytes>(it.key));
         __syncthreads();
+        GCM_MARK(3, idx);
         uint32_t rk[NW];
 #pragma unroll
         for (int i = 0; i < NW; ++i) rk[i] = __builtin_amdgcn_readfirstlane(lds<uint32_t>(kRk + 4 * i));
@@ -300,6 +309,7 @@ __global__ __launch_bounds__(kGcmThreads) void rc_gcm_kernel(GcmArgs a) {
         }
         __syncthreads();
 
+        GCM_MARK(4, idx);
         // ---- C: the nibble tables of H, H^32 and H^1024 (32 lanes each)
         if (wave < 3 && lane < 32) {
             const uint32_t src = wave == 0 ? kH : wave == 1 ? kH32 : kHM;
@@ -308,6 +318,7 @@ __global__ __launch_bounds__(kGcmThreads) void rc_gcm_kernel(GcmArgs a) {
         }
         __syncthreads();
 
+        GCM_MARK(5, idx);
         // ---- D: other nonce lengths: J0 = GHASH_H(IV || 0-pad || 0^64 || [len(IV)]_64)
         if (nbytes != 12) {
             if (tid == 0) {
@@ -337,6 +348,7 @@ __global__ __launch_bounds__(kGcmThreads) void rc_gcm_kernel(GcmArgs a) {
         const uint64_t rows = (nb + pad) / kGcmThreads;
         const bool fast = ((src_a | dst_a) & 3) == 0;
         u32x4 acc = {0u, 0u, 0u, 0u};
+        GCM_MARK(6, rows);
         for (uint64_t r = 0; r < rows; ++r) {
             const int64_t b = int64_t(r * kGcmThreads + uint64_t(tid)) - int64_t(pad);
             u32x4 x = {0u, 0u, 0u, 0u};
@@ -360,6 +372,7 @@ __global__ __launch_bounds__(kGcmThreads) void rc_gcm_kernel(GcmArgs a) {
         }
         lds<u32x4>(kZ + 16 * tid) = acc;
         __syncthreads();
+        GCM_MARK(7, rows);
 
         // ---- F: fold the chains: P_j = sum_i Z_(32j+i) H^(32-i); D = sum_j P_j H^(32(31-j))
         if (wave == 0 && lane < 32) {
@@ -369,6 +382,7 @@ __global__ __launch_bounds__(kGcmThreads) void rc_gcm_kernel(GcmArgs a) {
             lds<u32x4>(kP + 16 * lane) = p;
         }
         __syncthreads();
+        GCM_MARK(8, idx);
         if (tid == 0) {
             u32x4 d = lds<u32x4>(kP);
 #pragma unroll 1
@@ -383,7 +397,7 @@ __global__ __launch_bounds__(kGcmThreads) void rc_gcm_kernel(GcmArgs a) {
                 store_bytes(dst + len, tag, 16);
             }
         }
-        // the barrier at the top of the next item orders these LDS reads before its writes
+        GCM_MARK(10, idx);
     }
 }
 
@@ -424,6 +438,19 @@ int launch_nr(bool decrypt, const GcmArgs &args, unsigned groups, hipStream_t st
 }  // namespace
 
 const char *rc_gcm_launch_error(void) { return g_gcm_err; }
+
+#ifdef RC_GCM_TRACE
+int rc_gcm_trace_read(unsigned long long *out, hipStream_t st) {
+    if (hipMemcpyFromSymbolAsync(out, HIP_SYMBOL(g_gcm_trace), sizeof g_gcm_trace, 0,
+                                 hipMemcpyDeviceToHost, st) != hipSuccess)
+        return 1;
+    return hipStreamSynchronize(st) != hipSuccess;
+}
+int rc_gcm_trace_reset(void) {
+    const unsigned long long z[4] = {0, 0, 0, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_gcm_trace), z, sizeof z) != hipSuccess;
+}
+#endif
 
 int rc_gcm_launch(uint32_t key_bytes, bool decrypt, const GcmArgs &args, unsigned groups,
                   hipStream_t stream) {
