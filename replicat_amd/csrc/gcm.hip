@@ -87,6 +87,11 @@ __device__ __forceinline__ T &lds(uint32_t off) {
 __device__ __forceinline__ uint32_t rotl8(uint32_t x) { return (x << 8) | (x >> 24); }
 __device__ __forceinline__ uint32_t rot16(uint32_t x) { return __builtin_amdgcn_alignbit(x, x, 16); }
 __device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
+// a ^ b ^ c in one VALU (gfx950 v_bitop3_b32, truth table 0x96): the rounds and GHASH are
+// VALU-co-bound with the LDS, and half their XORs fold away
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
 
 // ------------------------------------------------------------------------------ AES
 
@@ -114,14 +119,14 @@ __device__ __forceinline__ u32x4 aes_encrypt(u32x4 in, const uint32_t *rk, uint3
 #pragma unroll
     for (int r = 1; r < NR; ++r) {
         // column c takes row k from column c + k (ShiftRows); T_k = rotl(8k) T0 (MixColumns)
-        const uint32_t n0 = tl(s0, lo0, sel(0)) ^ tl(s1, lo1, sel(1)) ^
-                            rot16(tl(s2, lo0, sel(2)) ^ tl(s3, lo1, sel(3)) ^ rk[4 * r]);
-        const uint32_t n1 = tl(s1, lo0, sel(0)) ^ tl(s2, lo1, sel(1)) ^
-                            rot16(tl(s3, lo0, sel(2)) ^ tl(s0, lo1, sel(3)) ^ rk[4 * r + 1]);
-        const uint32_t n2 = tl(s2, lo0, sel(0)) ^ tl(s3, lo1, sel(1)) ^
-                            rot16(tl(s0, lo0, sel(2)) ^ tl(s1, lo1, sel(3)) ^ rk[4 * r + 2]);
-        const uint32_t n3 = tl(s3, lo0, sel(0)) ^ tl(s0, lo1, sel(1)) ^
-                            rot16(tl(s1, lo0, sel(2)) ^ tl(s2, lo1, sel(3)) ^ rk[4 * r + 3]);
+        const uint32_t n0 = xor3(tl(s0, lo0, sel(0)), tl(s1, lo1, sel(1)),
+                                 rot16(xor3(tl(s2, lo0, sel(2)), tl(s3, lo1, sel(3)), rk[4 * r])));
+        const uint32_t n1 = xor3(tl(s1, lo0, sel(0)), tl(s2, lo1, sel(1)),
+                                 rot16(xor3(tl(s3, lo0, sel(2)), tl(s0, lo1, sel(3)), rk[4 * r + 1])));
+        const uint32_t n2 = xor3(tl(s2, lo0, sel(0)), tl(s3, lo1, sel(1)),
+                                 rot16(xor3(tl(s0, lo0, sel(2)), tl(s1, lo1, sel(3)), rk[4 * r + 2])));
+        const uint32_t n3 = xor3(tl(s3, lo0, sel(0)), tl(s0, lo1, sel(1)),
+                                 rot16(xor3(tl(s1, lo0, sel(2)), tl(s2, lo1, sel(3)), rk[4 * r + 3])));
         s0 = n0;
         s1 = n1;
         s2 = n2;
@@ -180,8 +185,10 @@ __device__ __forceinline__ u32x4 tab_mul(u32x4 x) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint32_t j = 2 * (4 * d + k);
-            acc ^= lds<u32x4>(BASE + j * 256 + ((hi >> (8 * k)) & 0xFFu));
-            acc ^= lds<u32x4>(BASE + (j + 1) * 256 + ((lo >> (8 * k)) & 0xFFu));
+            const u32x4 p = lds<u32x4>(BASE + j * 256 + ((hi >> (8 * k)) & 0xFFu));
+            const u32x4 q = lds<u32x4>(BASE + (j + 1) * 256 + ((lo >> (8 * k)) & 0xFFu));
+            acc = u32x4{xor3(acc.x, p.x, q.x), xor3(acc.y, p.y, q.y), xor3(acc.z, p.z, q.z),
+                        xor3(acc.w, p.w, q.w)};
         }
     }
     return acc;
