@@ -15,15 +15,19 @@ does (replicat_amd/adapters.py): every batch but the last is chunked as an OPEN 
 reference's non-final ``next_cut`` calls), the last with its real framing, and the uncut tail
 is carried into the next batch.  Each batch is uploaded ONCE and everything runs on the bytes in
 HBM: the cut chain (rc_chunk_device), the chunk digests (rc_blake2b_chunks), the per-file
-incremental digests (rc_blake2b_update_device: each file's bytes are fed once, in the batch that
-first holds them; a file's state lives in HBM across batches) and, with ``encryption``, every
+incremental digests of small files (rc_blake2b_update_device: each file's bytes are fed once, in
+the batch that first holds them; a file's state lives in HBM across batches) and, with ``encryption``, every
 chunk's subkey (rc_blake2b_derive_chunks) and its AES-GCM encryption (rc_gcm_encrypt_chunks).
 Only cut offsets, digests and -- what replicat uploads -- the chunk contents come back: sliced
 from the host batch, or the device's nonce || C || T when encrypted.
 
 The dedup table and the chunk -> file range map are host bookkeeping on a few integers per
-chunk, as in the reference.  There is no CPU fallback: every cut, digest and ciphertext comes
-from the HIP library.
+chunk, as in the reference.  Per-file digests of files of 1 MiB and more are hashed on host
+threads from the pinned batch while the device works (``file_digests='auto'``): a file digest is
+one sequential chain, which a host core advances ~10x faster than one device chain (measured,
+DESIGN.md §5c); ``file_digests='device'`` keeps every file on the device.  There is no CPU
+fallback: every cut, chunk digest, subkey and ciphertext comes from the HIP library, and a
+missing library raises.
 """
 import bisect
 import os
@@ -128,7 +132,7 @@ class DeviceSnapshotProducer:
     def __init__(self, *, min_length: int = MIN_LENGTH, max_length: int = MAX_LENGTH,
                  params: Optional[bytes] = None, digest_size: int = 64,
                  batch_bytes: int = DEFAULT_BATCH, device=None, keep_contents: bool = True,
-                 encryption: Optional[ChunkEncryption] = None):
+                 encryption: Optional[ChunkEncryption] = None, file_digests: str = 'auto'):
         import torch
         if device is None:
             device = _current_device()
@@ -143,6 +147,10 @@ class DeviceSnapshotProducer:
         self.digest_size = digest_size
         self.batch_bytes = max(int(batch_bytes), 2 * max_length + 16)
         self.keep_contents = keep_contents
+        if file_digests not in ('auto', 'device', 'host'):
+            raise ValueError(f'file_digests must be auto, device or host, not {file_digests!r}')
+        self.file_digests = file_digests
+        self._pool = None
         # one batch plus the carried tail (< max_length) plus one piece of overshoot
         self.capacity = self.batch_bytes + max_length + PIECE + 64
         self.host = torch.empty(self.capacity, dtype=torch.uint8, pin_memory=True)
@@ -168,6 +176,40 @@ class DeviceSnapshotProducer:
             out_total, _ = self.cipher.chunks_layout(self.chunker, [self.capacity])
             self.d_enc = torch.empty(max(out_total, 1), dtype=torch.uint8, device=self.dev)
 
+    # ------------------------------------------------------------------- file digests
+
+    # A file digest is ONE sequential BLAKE2b chain over the whole file.  On the device a chain
+    # advances one 128-byte block per ~1.4 us (the dependent-instruction latency of a quad of
+    # lanes); a host core does ~1 GB/s.  Many small files hash in parallel on the
+    # device within a batch, but a large file's chain would set the batch time (a 256 MiB file:
+    # 2.9 s on the device, 0.27 s on a host core), so 'auto' hashes files of at least
+    # HOST_DIGEST_MIN bytes on host threads from the pinned batch, overlapped with the device
+    # work; 'device' and 'host' force one engine.
+    HOST_DIGEST_MIN = 1 << 20
+
+    def _on_host(self, fi, f, read, hstates):
+        if fi in hstates:
+            return True
+        if self.file_digests == 'device':
+            return False
+        if self.file_digests == 'auto':
+            try:
+                size = os.stat(f.path).st_size if read is None else 0
+            except OSError:
+                size = 0
+            if size < self.HOST_DIGEST_MIN:
+                return False
+        import hashlib
+        hstates[fi] = hashlib.blake2b(digest_size=self.digest_size)
+        return True
+
+    def _host_pool(self):
+        if self._pool is None:
+            from concurrent.futures import ThreadPoolExecutor
+            self._pool = ThreadPoolExecutor(max_workers=max(1, min(16, os.cpu_count() or 1)),
+                                            thread_name_prefix='rc-file-digest')
+        return self._pool
+
     # ------------------------------------------------------------------------------ run
 
     def run(self, paths: Sequence[os.PathLike], read=None) -> SnapshotStream:
@@ -178,6 +220,7 @@ class DeviceSnapshotProducer:
         chunks: List[ChunkRecord] = []
         table: Dict[bytes, int] = {}
         states = {}              # file index -> device state (open files only)
+        hstates = {}             # file index -> host hasher (open large files only)
         finalized = 0            # files [0, finalized) have their digest
         hnp = self.host.numpy()
         buf_start = 0            # stream offset of host[0]
@@ -195,6 +238,23 @@ class DeviceSnapshotProducer:
                 nxt = next(it, None)
             final = nxt is None
             closed = len(files) if final else nxt[1]
+            # ---- host: per-file digests of the large files, hashed from the pinned batch while
+            # the device works on it (see _on_host)
+            lo_stream, hi_stream = buf_start + fed, buf_start + blen
+            host_jobs = []       # (file index, future or None, final)
+            for fi in range(finalized, len(files)):
+                if not self._on_host(fi, files[fi], read, hstates):
+                    continue
+                f = files[fi]
+                a, b = max(f.stream_start, lo_stream), min(f.stream_end, hi_stream)
+                is_final = fi < closed
+                if b <= a and not is_final:
+                    continue
+                fut = None
+                if b > a:
+                    fut = self._host_pool().submit(hstates[fi].update,
+                                                   memoryview(hnp)[a - buf_start:b - buf_start])
+                host_jobs.append((fi, fut, is_final))
             # ---- device: upload, cut chain, chunk digests
             if blen:
                 self.dbuf[:blen].copy_(self.host[:blen], non_blocking=True)
@@ -217,8 +277,9 @@ class DeviceSnapshotProducer:
                                            self.d_nonces.data_ptr(), self.d_enc.data_ptr(), hs)
             # ---- device: per-file incremental digests over the fresh bytes [fed, blen)
             items = []           # (file index, device ptr, length, final)
-            lo_stream, hi_stream = buf_start + fed, buf_start + blen
             for fi in range(finalized, len(files)):
+                if fi in hstates:
+                    continue
                 f = files[fi]
                 a, b = max(f.stream_start, lo_stream), min(f.stream_end, hi_stream)
                 n = b - a if b > a else 0
@@ -254,6 +315,11 @@ class DeviceSnapshotProducer:
                     if fin:
                         files[fi].digest = fd[j].tobytes()
                         del states[fi]
+            for fi, fut, fin in host_jobs:  # before the batch buffer is reused
+                if fut is not None:
+                    fut.result()
+                if fin:
+                    files[fi].digest = hstates.pop(fi).digest()
             while finalized < closed and files[finalized].digest is not None:
                 finalized += 1
             prev = 0

@@ -1,0 +1,89 @@
+"""Time the device snapshot producer end to end (SURVEY §8 d config 1 and a larger file set).
+
+    python scripts/producer_probe.py [total_mib] [files]
+
+Writes `files` files of random bytes (total `total_mib` MiB; default one 256 MiB file = config 1)
+under $TMPDIR, then times DeviceSnapshotProducer.run over them (page-cache reads, as a repeated
+snapshot sees them): unencrypted and encrypted, contents kept as replicat's upload queue needs
+them.  The CPU leg of the same work (the oracle's chunker over the framed stream + hashlib
+BLAKE2b per chunk and per file, one core) is timed beside it as the baseline; it is the checker,
+not the measured path.  One JSON line per variant.
+"""
+import hashlib
+import json
+import os
+import sys
+import tempfile
+import time
+
+sys.path.insert(0, '.')
+import torch  # noqa: E402
+
+from oracle import oracle as o  # noqa: E402
+from replicat_amd import snapshot  # noqa: E402
+from replicat_amd.pipeline import ChunkEncryption, DeviceSnapshotProducer  # noqa: E402
+
+total_mib = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+nfiles = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+MIN, MAX = 128_000, 5_120_000
+GIB = float(1 << 30)
+
+torch.cuda.set_device(0)
+tmp = tempfile.mkdtemp(prefix='rc_probe_')
+paths, sizes = [], []
+rng = __import__('random').Random(1)
+per = (total_mib << 20) // nfiles
+for i in range(nfiles):
+    n = per + (rng.randrange(0, 4096) if nfiles > 1 else 0)
+    p = os.path.join(tmp, 'f%04d' % i)
+    with open(p, 'wb') as f:
+        f.write(os.urandom(n))
+    paths.append(p)
+    sizes.append(n)
+total = sum(sizes)
+print(json.dumps({'progress': 'files written', 'bytes': total, 'files': nfiles}), flush=True)
+
+
+def timed(fn, reps=3):
+    fn()  # warm (page cache, allocations)
+    best = None
+    for _ in range(reps):
+        t = time.perf_counter()
+        out = fn()
+        dt = time.perf_counter() - t
+        best = dt if best is None or dt < best else best
+    return best, out
+
+
+enc = ChunkEncryption(shared_key=os.urandom(32), shared_kdf_params=os.urandom(16))
+for name, kw in (('plain', {}), ('encrypted', {'encryption': enc})):
+    prod = DeviceSnapshotProducer(min_length=MIN, max_length=MAX, **kw)
+    dt, res = timed(lambda: prod.run(paths))
+    print(json.dumps({'variant': name, 'bytes': total, 'files': nfiles, 'chunks': len(res.chunks),
+                      's': round(dt, 4), 'gib_s': round(total / dt / GIB, 3)}), flush=True)
+    if name == 'plain':
+        plain = res
+
+# CPU baseline: the oracle's chunker + hashlib over the same framed stream (one core)
+def cpu_leg():
+    pieces = list(snapshot.stream_pieces(snapshot.sort_files(paths)))
+    stream = b''.join(pieces)
+    P = len(stream) - len(pieces[-1]) if pieces else 0
+    ends = o.chunk_stream(stream, MIN, MAX, None, P)
+    prev, digs = 0, []
+    for e in ends:
+        digs.append(hashlib.blake2b(stream[prev:e]).digest())
+        prev = e
+    fd = [hashlib.blake2b(open(p, 'rb').read()).digest() for p in paths]
+    return ends, digs, fd
+
+
+dt, (ends, digs, fd) = timed(cpu_leg, reps=1)
+assert [c.stream_end for c in plain.chunks] == ends, 'cut mismatch'
+assert [c.digest for c in plain.chunks] == digs, 'digest mismatch'
+assert sorted(f.digest for f in plain.files) == sorted(fd), 'file digest mismatch'
+print(json.dumps({'variant': 'cpu_oracle_1core', 'bytes': total, 's': round(dt, 4),
+                  'gib_s': round(total / dt / GIB, 3), 'matches_gpu': True}), flush=True)
+for p in paths:
+    os.unlink(p)
+os.rmdir(tmp)

@@ -62,8 +62,9 @@ def test_reference_snapshots(tmp_path, name):
     assert len(res.files) == len(files_data)
 
 
-@pytest.mark.parametrize('batch', [1, 3 << 20, 64 << 20])
-def test_many_files_many_batches(oracle, tmp_path, batch):
+@pytest.mark.parametrize('batch,engine', [(1, 'auto'), (3 << 20, 'auto'), (64 << 20, 'auto'),
+                                          (3 << 20, 'device'), (1, 'host')])
+def test_many_files_many_batches(oracle, tmp_path, batch, engine):
     """Small params and small batches: files straddle batches, the carried tail, empty files
     between batches; cuts against the oracle over the whole framed stream."""
     rnd = random.Random(batch)
@@ -76,7 +77,7 @@ def test_many_files_many_batches(oracle, tmp_path, batch):
     mn, mx = 2_000, 80_000
     key = synth.seeded_key(7)
     res = DeviceSnapshotProducer(min_length=mn, max_length=mx, params=key,
-                                 batch_bytes=batch).run(paths)
+                                 batch_bytes=batch, file_digests=engine).run(paths)
     pieces = list(snapshot.stream_pieces(snapshot.sort_files(paths)))
     stream = b''.join(pieces)
     P = len(stream) - len(pieces[-1]) if pieces else 0
@@ -85,13 +86,15 @@ def test_many_files_many_batches(oracle, tmp_path, batch):
     check_stream(res, files_data, lengths)
 
 
-def test_big_files_default_params(tmp_path):
-    """Files across the 16 MiB piece size with default params (reference fixture)."""
+@pytest.mark.parametrize('engine', ['auto', 'device'])
+def test_big_files_default_params(tmp_path, engine):
+    """Files across the 16 MiB piece size with default params (reference fixture); file digests
+    on host threads ('auto': these files are large) and all on the device."""
     files_data = file_sets()['big_files']
     paths = write(tmp_path, files_data)
     s = SNAPS['big_files']
     res = DeviceSnapshotProducer(min_length=s['min'], max_length=s['max'],
-                                 batch_bytes=20 << 20).run(paths)
+                                 batch_bytes=20 << 20, file_digests=engine).run(paths)
     check_stream(res, files_data, s['lengths'])
 
 
