@@ -31,6 +31,7 @@ missing library raises.
 """
 import bisect
 import os
+import time
 from dataclasses import dataclass, field
 from typing import Dict, Iterator, List, Optional, Sequence, Tuple
 
@@ -40,7 +41,10 @@ from .chunker import MAX_LENGTH, MIN_LENGTH, GpuChunker, _current_device, normal
 from .hashing import SLOT, STATE_BYTES, GpuBlake2b, state_init
 from .snapshot import ALIGNMENT, PIECE, sort_files
 
-DEFAULT_BATCH = 256 << 20
+# The device time of a batch has a floor: the BLAKE2b chain of its longest chunk (~55 ms for a
+# 5.12 MB chunk), whatever the batch size; 1 GiB batches amortize it (256 MiB ones
+# spent ~58 ms per batch on the device, measured).
+DEFAULT_BATCH = 1 << 30
 
 
 @dataclass
@@ -175,6 +179,7 @@ class DeviceSnapshotProducer:
             self.d_nonces = torch.empty(max(total, 1) * nb, dtype=torch.uint8, device=self.dev)
             out_total, _ = self.cipher.chunks_layout(self.chunker, [self.capacity])
             self.d_enc = torch.empty(max(out_total, 1), dtype=torch.uint8, device=self.dev)
+            self.h_enc = torch.empty(max(out_total, 1), dtype=torch.uint8, pin_memory=True)
 
     # ------------------------------------------------------------------- file digests
 
@@ -228,7 +233,12 @@ class DeviceSnapshotProducer:
         fed = 0                  # host[0:fed] already fed to the file digests
         it = tagged_pieces(sort_files(paths), files, read)
         nxt = next(it, None)
+        prof = self.profile = {'fill': 0.0, 'device': 0.0, 'host_digest_wait': 0.0, 'records': 0.0,
+                               'batches': 0}
+        clock = time.perf_counter
         while True:
+            t0 = clock()
+            prof['batches'] += 1
             last_start = blen
             while nxt is not None and (blen < self.batch_bytes or blen == 0):
                 piece, _ = nxt
@@ -238,6 +248,8 @@ class DeviceSnapshotProducer:
                 nxt = next(it, None)
             final = nxt is None
             closed = len(files) if final else nxt[1]
+            t1 = clock()
+            prof['fill'] += t1 - t0
             # ---- host: per-file digests of the large files, hashed from the pinned batch while
             # the device works on it (see _on_host)
             lo_stream, hi_stream = buf_start + fed, buf_start + blen
@@ -308,18 +320,24 @@ class DeviceSnapshotProducer:
             if self.encryption is not None:
                 over = self.cipher.nonce_bytes + 16
                 n_out = (int(ends[-1]) if count else 0) + count * over
-                enc = self.d_enc[:n_out].cpu().numpy()
+                self.h_enc[:n_out].copy_(self.d_enc[:n_out], non_blocking=True)
+                stream.synchronize()
+                enc = self.h_enc[:n_out].numpy()
             if file_digests is not None:
                 fd = file_digests[:, :self.digest_size].cpu().numpy()
                 for j, (fi, _, _, fin) in enumerate(items):
                     if fin:
                         files[fi].digest = fd[j].tobytes()
                         del states[fi]
+            t2 = clock()
+            prof['device'] += t2 - t1
             for fi, fut, fin in host_jobs:  # before the batch buffer is reused
                 if fut is not None:
                     fut.result()
                 if fin:
                     files[fi].digest = hstates.pop(fi).digest()
+            t3 = clock()
+            prof['host_digest_wait'] += t3 - t2
             while finalized < closed and files[finalized].digest is not None:
                 finalized += 1
             prev = 0
@@ -337,6 +355,7 @@ class DeviceSnapshotProducer:
                                           stream_end=buf_start + e, digest=d, table_index=idx,
                                           contents=contents))
                 prev = e
+            prof['records'] += clock() - t3
             if final:
                 if prev != blen:
                     raise RuntimeError(f'final batch left {blen - prev} bytes uncut')

@@ -60,7 +60,8 @@ for name, kw in (('plain', {}), ('encrypted', {'encryption': enc})):
     prod = DeviceSnapshotProducer(min_length=MIN, max_length=MAX, **kw)
     dt, res = timed(lambda: prod.run(paths))
     print(json.dumps({'variant': name, 'bytes': total, 'files': nfiles, 'chunks': len(res.chunks),
-                      's': round(dt, 4), 'gib_s': round(total / dt / GIB, 3)}), flush=True)
+                      's': round(dt, 4), 'gib_s': round(total / dt / GIB, 3),
+                      'phases_s': {k: round(v, 4) for k, v in prod.profile.items()}}), flush=True)
     if name == 'plain':
         plain = res
 
