@@ -1,6 +1,7 @@
 """Build libreplicat_chunker.so in-tree: hipcc, gfx950 only, no torch extension machinery.
 
     python -m replicat_amd.build        (also run by __graft_entry__.build())
+    python -m replicat_amd.build --diag (+ the GCM watchdog harness under diag/)
 """
 import os
 import shutil
@@ -44,5 +45,22 @@ def build(force=False, verbose=False):
     return LIB
 
 
+def build_diag(verbose=False):
+    """The AES-GCM watchdog harness (scripts/gcm_diag.cpp) as two executables under diag/: on the
+    production kernel, and with -DRC_GCM_TRACE (a progress word the host polls while the kernel
+    runs).  Diagnostics only; nothing in the product loads them."""
+    out_dir = os.path.join(ROOT, 'diag')
+    os.makedirs(out_dir, exist_ok=True)
+    srcs = SOURCES + [os.path.join(ROOT, 'scripts', 'gcm_diag.cpp')]
+    for name, extra in (('gcm_diag_notrace', []), ('gcm_diag', ['-DRC_GCM_TRACE'])):
+        cmd = [hipcc(), f'--offload-arch={ARCH}', '-O3', '-std=c++17', *extra,
+               '-I', os.path.join(ROOT, 'include'), *srcs, '-o', os.path.join(out_dir, name)]
+        if verbose:
+            print(' '.join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+
+
 if __name__ == '__main__':
     build(force='--force' in sys.argv, verbose=True)
+    if '--diag' in sys.argv:
+        build_diag(verbose=True)
