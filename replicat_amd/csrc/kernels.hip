@@ -583,6 +583,7 @@ struct EdgeRange {
     const uint8_t *p;     // word q0 of the stream
     uint64_t a, q0;       // first key, first word of iteration 0 (a & ~3)
     uint32_t nk, wlast;   // last key offset from q0, last existing word from q0
+    uint32_t lo, span;    // valid key offsets: lo = a - q0 (0-3) .. nk, as off - lo <= span
     uint32_t it0;         // next iteration to load
     uint32_t carry;       // entry of the word before the next iteration's lane 0 key
     uint32_t carry_word;
@@ -595,6 +596,8 @@ struct EdgeRange {
         a = a_;
         q0 = a_ & ~3ull;
         nk = live ? (uint32_t)(b_ - q0) : 0;
+        lo = (uint32_t)(a_ - q0);
+        span = nk - lo;  // live: b >= a, so nk >= lo
         p = base + 4 * q0;
         wlast = live ? (uint32_t)(wmax - q0) : 0;
         it0 = 0;
@@ -637,10 +640,11 @@ struct EdgeRange {
             carry = rot;
             const uint32_t t[4] = {(ep & 0xffff0000u) ^ (e0 << 16), (e0 & 0xffff0000u) ^ (e1 << 16),
                                    (e1 & 0xffff0000u) ^ (e2 << 16), (e2 & 0xffff0000u) ^ (e3 << 16)};
+            // one 32-bit compare per key: off < lo wraps above span
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const uint32_t off = it * 256 + lane * 4 + k;  // key q0 + off
-                const bool valid = off <= nk && q0 + off >= a;
+                const bool valid = off - lo <= span;
                 const uint32_t local = 256u * R + it * 4 + k;
                 acc_first = max3_u32(acc_first, valid ? (t[k] | 0x8000u | (511u - local)) : 0u, 0u);
                 acc_last = max3_u32(acc_last, valid ? (t[k] | 0x8000u | local) : 0u, 0u);
