@@ -640,6 +640,17 @@ struct EdgeRange {
             carry = rot;
             const uint32_t t[4] = {(ep & 0xffff0000u) ^ (e0 << 16), (e0 & 0xffff0000u) ^ (e1 << 16),
                                    (e1 & 0xffff0000u) ^ (e2 << 16), (e2 & 0xffff0000u) ^ (e3 << 16)};
+            // an iteration whose 256 keys are all in range (every one but the first and the
+            // last, as a rule) skips the per-key test and folds two keys per v_max3
+            const uint32_t it_lo = it * 256u, it_hi = it * 256u + 255u;
+            if (it_lo >= lo && it_hi <= nk) {
+                const uint32_t lf = 511u - 256u * R - it * 4u, ll = 256u * R + it * 4u;
+                acc_first = max3_u32(acc_first, t[0] | 0x8000u | lf, t[1] | 0x8000u | (lf - 1u));
+                acc_first = max3_u32(acc_first, t[2] | 0x8000u | (lf - 2u), t[3] | 0x8000u | (lf - 3u));
+                acc_last = max3_u32(acc_last, t[0] | 0x8000u | ll, t[1] | 0x8000u | (ll + 1u));
+                acc_last = max3_u32(acc_last, t[2] | 0x8000u | (ll + 2u), t[3] | 0x8000u | (ll + 3u));
+                continue;
+            }
             // one 32-bit compare per key: off < lo wraps above span
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
