@@ -571,7 +571,7 @@ __device__ __forceinline__ ChainStream chain_stream(const StreamDesc &d, uint64_
 // (top16 << 16 | valid 0x8000 | order) for the first and the last occurrence; the order is the
 // lane-local key index (0-255 head, 256-511 tail; a range holds at most 8190 keys).
 #ifndef RC_EDGE_ITERS
-#define RC_EDGE_ITERS 4
+#define RC_EDGE_ITERS 2
 #endif
 constexpr int kEdgeIters = RC_EDGE_ITERS;  // 256-key iterations whose loads are issued together
 
@@ -737,13 +737,19 @@ __device__ int chain_step(const uint64_t *tl, const uint64_t *th, const TileReco
             }
             wave_best(bk, bj);
             RC_STAMP(2);
+            // a range's next batch is issued as soon as its registers are consumed, so the
+            // other range's compute covers its latency
             for (;;) {
                 const bool m0 = r0.more(), m1 = r1.more();
                 if (!m0 && !m1) break;
-                if (m0) r0.compute(w0, lb_a, lb_b, acc_first, acc_last);
-                if (m1) r1.compute(w1, lb_a, lb_b, acc_first, acc_last);
-                if (r0.more()) r0.load(w0);
-                if (r1.more()) r1.load(w1);
+                if (m0) {
+                    r0.compute(w0, lb_a, lb_b, acc_first, acc_last);
+                    if (r0.more()) r0.load(w0);
+                }
+                if (m1) {
+                    r1.compute(w1, lb_a, lb_b, acc_first, acc_last);
+                    if (r1.more()) r1.load(w1);
+                }
             }
             RC_STAMP(3);
             const uint32_t m = wave_max_u32(acc_first);
