@@ -725,6 +725,16 @@ __device__ int chain_step(const uint64_t *tl, const uint64_t *th, const TileReco
 #pragma unroll
                 for (int u = 0; u < kRecUnroll; ++u) rv[u] = rec[min(rlo + 64 * u + lane_id(), rhi - 1)];
             }
+            // An edge range inside one tile needs no scan when that tile's record -- its FIRST
+            // maximal key -- lies in the range (the first maximum of a set is the first maximum
+            // of every subset holding it), or when the tile's keys are all 0 (never taken,
+            // adapters.cpp:60-63).  The records come with the same round trip; the range's
+            // first batch is issued anyway and simply not consumed.
+            const bool one0 = r0.live && a0 / kTileKeys == b0 / kTileKeys;
+            const bool one1 = r1.live && a1 / kTileKeys == b1 / kTileKeys;
+            TileRecord er0 = {}, er1 = {};
+            if (one0) er0 = rec[st.tb0 + a0 / kTileKeys];
+            if (one1) er1 = rec[st.tb0 + a1 / kTileKeys];
             if (r0.more()) r0.load(w0);
             if (r1.more()) r1.load(w1);
             if (have_rec) {
@@ -734,6 +744,14 @@ __device__ int chain_step(const uint64_t *tl, const uint64_t *th, const TileReco
                         take_best(rv[u].key, rv[u].j, bk, bj);
                 if (rhi - rlo > 64 * kRecUnroll)  // windows beyond 512 tiles (max > 8 MiB)
                     scan_records(rec, rlo + 64 * kRecUnroll, rhi, bk, bj);
+            }
+            if (one0 && (er0.key == 0 || (er0.j >= a0 && er0.j <= b0))) {
+                if (er0.key != 0) take_best(er0.key, er0.j, bk, bj);
+                r0.live = false;
+            }
+            if (one1 && (er1.key == 0 || (er1.j >= a1 && er1.j <= b1))) {
+                if (er1.key != 0) take_best(er1.key, er1.j, bk, bj);
+                r1.live = false;
             }
             wave_best(bk, bj);
             RC_STAMP(2);
