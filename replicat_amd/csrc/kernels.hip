@@ -745,15 +745,19 @@ __device__ int chain_step(const uint64_t *tl, const uint64_t *th, const TileReco
                 if (rhi - rlo > 64 * kRecUnroll)  // windows beyond 512 tiles (max > 8 MiB)
                     scan_records(rec, rlo + 64 * kRecUnroll, rhi, bk, bj);
             }
-            if (one0 && (er0.key == 0 || (er0.j >= a0 && er0.j <= b0))) {
-                if (er0.key != 0) take_best(er0.key, er0.j, bk, bj);
+            wave_best(bk, bj);
+            // Otherwise the record still bounds the range from above: the head range (indices
+            // below every full tile's) cannot win when its bound is below the records' best,
+            // the tail range (indices above) not even when it equals it (index asc breaks the
+            // tie) -- and the final best is at least the records' best.
+            if (one0 && (er0.key == 0 || (er0.j >= a0 && er0.j <= b0) || er0.key < bk)) {
+                if (er0.key != 0 && er0.j >= a0 && er0.j <= b0) take_best(er0.key, er0.j, bk, bj);
                 r0.live = false;
             }
-            if (one1 && (er1.key == 0 || (er1.j >= a1 && er1.j <= b1))) {
-                if (er1.key != 0) take_best(er1.key, er1.j, bk, bj);
+            if (one1 && (er1.key == 0 || (er1.j >= a1 && er1.j <= b1) || er1.key <= bk)) {
+                if (er1.key != 0 && er1.j >= a1 && er1.j <= b1) take_best(er1.key, er1.j, bk, bj);
                 r1.live = false;
             }
-            wave_best(bk, bj);
             RC_STAMP(2);
             // a range's next batch is issued as soon as its registers are consumed, so the
             // other range's compute covers its latency
