@@ -601,7 +601,7 @@ struct EdgeRange {
         p = base + 4 * q0;
         wlast = live ? (uint32_t)(wmax - q0) : 0;
         it0 = 0;
-        carry_word = live ? ld_u32(base + 4 * (q0 ? q0 - 1 : 0)) : 0;
+        carry_word = 0;  // loaded with the first batch
         carry = 0;
     }
     __device__ bool more() const { return live && it0 * 256 <= nk; }
@@ -609,8 +609,9 @@ struct EdgeRange {
     // clamped to the aligned block holding the last existing word: past the stream's end the
     // lane's keys are invalid anyway, and a 16-byte block that holds a stream byte cannot
     // cross a page, so the read is safe even with no padding after the stream.
-    __device__ void load(uint32_t (&w)[kEdgeIters][4]) const {
+    __device__ void load(uint32_t (&w)[kEdgeIters][4]) {
         const uint32_t lane = lane_id();
+        if (it0 == 0) carry_word = ld_u32(q0 ? p - 4 : p);
 #pragma unroll
         for (int i = 0; i < kEdgeIters; ++i) {
             const uint32_t o = min((it0 + i) * 256 + lane * 4, wlast & ~3u);
@@ -713,7 +714,7 @@ __device__ int chain_step(const uint64_t *tl, const uint64_t *th, const TileReco
                 a1 = t_hi * kTileKeys;
                 b1 = jb;
             }
-            // one round trip: the records and both edge ranges' first batches in flight
+            // one round trip: the window's records and both edge tiles' records in flight
             EdgeRange r0, r1;
             r0.init(st.base, st.L / 4 - 1, a0, b0, 0);
             r1.init(st.base, st.L / 4 - 1, a1, b1, 1);
@@ -728,15 +729,12 @@ __device__ int chain_step(const uint64_t *tl, const uint64_t *th, const TileReco
             // An edge range inside one tile needs no scan when that tile's record -- its FIRST
             // maximal key -- lies in the range (the first maximum of a set is the first maximum
             // of every subset holding it), or when the tile's keys are all 0 (never taken,
-            // adapters.cpp:60-63).  The records come with the same round trip; the range's
-            // first batch is issued anyway and simply not consumed.
+            // adapters.cpp:60-63).  These records come with the window's, in one round trip.
             const bool one0 = r0.live && a0 / kTileKeys == b0 / kTileKeys;
             const bool one1 = r1.live && a1 / kTileKeys == b1 / kTileKeys;
             TileRecord er0 = {}, er1 = {};
             if (one0) er0 = rec[st.tb0 + a0 / kTileKeys];
             if (one1) er1 = rec[st.tb0 + a1 / kTileKeys];
-            if (r0.more()) r0.load(w0);
-            if (r1.more()) r1.load(w1);
             if (have_rec) {
 #pragma unroll
                 for (int u = 0; u < kRecUnroll; ++u)
@@ -758,6 +756,10 @@ __device__ int chain_step(const uint64_t *tl, const uint64_t *th, const TileReco
                 if (er1.key != 0 && er1.j >= a1 && er1.j <= b1) take_best(er1.key, er1.j, bk, bj);
                 r1.live = false;
             }
+            // the few ranges left are scanned: their first batches only now (a second round
+            // trip for them; none at all for the rest)
+            if (r0.more()) r0.load(w0);
+            if (r1.more()) r1.load(w1);
             RC_STAMP(2);
             // a range's next batch is issued as soon as its registers are consumed, so the
             // other range's compute covers its latency
