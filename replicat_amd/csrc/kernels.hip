@@ -722,10 +722,12 @@ __device__ int chain_step(const uint64_t *tl, const uint64_t *th, const TileReco
             uint32_t acc_first = 0, acc_last = 0;
             TileRecord rv[kRecUnroll];
             const uint64_t rlo = st.tb0 + t_lo, rhi = st.tb0 + t_hi;
-            if (have_rec) {
+            // only as many 64-record rows as the window has tiles (one for max_length up to
+            // 512 KiB; a default window has 625 tiles and takes all kRecUnroll and the loop)
+            const uint64_t nrow = have_rec ? min((rhi - rlo + 63) / 64, (uint64_t)kRecUnroll) : 0;
 #pragma unroll
-                for (int u = 0; u < kRecUnroll; ++u) rv[u] = rec[min(rlo + 64 * u + lane_id(), rhi - 1)];
-            }
+            for (int u = 0; u < kRecUnroll; ++u)
+                if ((uint64_t)u < nrow) rv[u] = rec[min(rlo + 64 * u + lane_id(), rhi - 1)];
             // An edge range inside one tile needs no scan when that tile's record -- its FIRST
             // maximal key -- lies in the range (the first maximum of a set is the first maximum
             // of every subset holding it), or when the tile's keys are all 0 (never taken,
@@ -738,7 +740,7 @@ __device__ int chain_step(const uint64_t *tl, const uint64_t *th, const TileReco
             if (have_rec) {
 #pragma unroll
                 for (int u = 0; u < kRecUnroll; ++u)
-                    if (rlo + 64 * u + lane_id() < rhi && rv[u].key != 0)
+                    if ((uint64_t)u < nrow && rlo + 64 * u + lane_id() < rhi && rv[u].key != 0)
                         take_best(rv[u].key, rv[u].j, bk, bj);
                 if (rhi - rlo > 64 * kRecUnroll)  // windows beyond 512 tiles (max > 8 MiB)
                     scan_records(rec, rlo + 64 * kRecUnroll, rhi, bk, bj);
