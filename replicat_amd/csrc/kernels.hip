@@ -98,17 +98,39 @@ __device__ __forceinline__ uint64_t full_key(const uint64_t *__restrict__ tl,
            th[512 + ((whi >> 16) & 255)] ^ th[768 + (whi >> 24)];
 }
 
-// (key desc, index asc) maximum over the wave; every lane gets the result.
-__device__ __forceinline__ void wave_best(uint64_t &k, uint64_t &j) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        const uint64_t ko = __shfl_xor(k, off);
-        const uint64_t jo = __shfl_xor(j, off);
-        if (ko > k || (ko == k && jo < j)) {
-            k = ko;
-            j = jo;
-        }
+// 64-bit DPP move; lanes without a source (bound_ctrl off, masked rows) keep their own value,
+// which the lexicographic maximum below absorbs.
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ uint64_t dpp_u64(uint64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)v, (int)(uint32_t)v,
+                                                              kCtrl, kRowMask, 0xf, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)(v >> 32),
+                                                              (int)(uint32_t)(v >> 32), kCtrl,
+                                                              kRowMask, 0xf, false);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ void best_step(uint64_t &k, uint64_t &j) {
+    const uint64_t ko = dpp_u64<kCtrl, kRowMask>(k), jo = dpp_u64<kCtrl, kRowMask>(j);
+    if (ko > k || (ko == k && jo < j)) {
+        k = ko;
+        j = jo;
     }
+}
+
+// (key desc, index asc) maximum over the wave; every lane gets the result.  DPP row shifts
+// 1/2/4/8 leave each row's maximum in its lane 15, row broadcasts 15 and 31 carry it to lane
+// 63, read back as a scalar: no LDS round trips (ds_bpermute) on the chain's critical path.
+__device__ __forceinline__ void wave_best(uint64_t &k, uint64_t &j) {
+    best_step<0x111, 0xf>(k, j);  // row_shr:1
+    best_step<0x112, 0xf>(k, j);  // row_shr:2
+    best_step<0x114, 0xf>(k, j);  // row_shr:4
+    best_step<0x118, 0xf>(k, j);  // row_shr:8
+    best_step<0x142, 0xa>(k, j);  // row_bcast:15 into rows 1 and 3
+    best_step<0x143, 0xc>(k, j);  // row_bcast:31 into rows 2 and 3
+    k = lane_u64(k, 63);
+    j = lane_u64(j, 63);
 }
 
 // ------------------------------------------------------------------ phase A: tile kernel
