@@ -162,6 +162,26 @@ __device__ __forceinline__ uint32_t pf_entry(uint32_t w, uint32_t lb_a, uint32_t
     return pf_lds(a0) ^ pf_lds(a1 + 128) ^ pf_lds(a2) ^ pf_lds(a3 + 128);
 }
 
+// The chain kernels' tables: the prefilter entries PF[4][256] once (no replication: the chain
+// scans an edge range only when the tile records cannot settle it, a few % of ranges), then
+// the exact TL/TH tables -- 20 KiB instead of 144 KiB, so several chain workgroups share a CU.
+__shared__ __attribute__((aligned(16))) uint32_t s_chain_lds[1024 + 4096];
+
+__device__ __forceinline__ uint32_t pfc_entry(const uint32_t *pf, uint32_t w) {
+    return pf[w & 255] ^ pf[256 + ((w >> 8) & 255)] ^ pf[512 + ((w >> 16) & 255)] ^
+           pf[768 + (w >> 24)];
+}
+
+__device__ __forceinline__ void stage_chain_tables(const KeyTables *tab) {
+    const uint32_t nt = blockDim.x;
+    const uint32_t *gpf = &tab->pf[0][0];
+    for (uint32_t i = threadIdx.x; i < 1024u; i += nt) s_chain_lds[i] = gpf[i];
+    uint64_t *full = reinterpret_cast<uint64_t *>(s_chain_lds + 1024);
+    const uint64_t *gfull = &tab->tl[0][0];
+    for (uint32_t i = threadIdx.x; i < 2048u; i += nt) full[i] = gfull[i];
+    __syncthreads();
+}
+
 // (key desc, index asc) improvement test: the lexicographic order makes the merge of ranges
 // and records independent of the order in which a lane visits them.
 __device__ __forceinline__ void take_best(uint64_t k, uint64_t j, uint64_t &bk, uint64_t &bj) {
@@ -644,20 +664,33 @@ struct EdgeRange {
             w[i][3] = v.w;
         }
     }
+    // kCompact: entries from the chain kernels' single PF copy at `pf`; otherwise from the
+    // tile kernel's 32x-replicated, conflict-free image
+    template <bool kCompact>
     __device__ void compute(const uint32_t (&w)[kEdgeIters][4], uint32_t lb_a, uint32_t lb_b,
-                            uint32_t &acc_first, uint32_t &acc_last) {
+                            const uint32_t *pf, uint32_t &acc_first, uint32_t &acc_last) {
         const uint32_t lane = lane_id();
-        if (it0 == 0) carry = pf_entry(carry_word, lb_a, lb_b);
+        if (it0 == 0) carry = kCompact ? pfc_entry(pf, carry_word) : pf_entry(carry_word, lb_a, lb_b);
 #pragma unroll
         for (int i = 0; i < kEdgeIters; ++i) {
             const uint32_t it = it0 + i;
-            uint32_t ad[16];
-            pf_addrs(w[i][0], lb_a, lb_b, ad + 0);
-            pf_addrs(w[i][1], lb_a, lb_b, ad + 4);
-            pf_addrs(w[i][2], lb_a, lb_b, ad + 8);
-            pf_addrs(w[i][3], lb_a, lb_b, ad + 12);
-            const uint32_t e0 = pf_gather(ad + 0), e1 = pf_gather(ad + 4);
-            const uint32_t e2 = pf_gather(ad + 8), e3 = pf_gather(ad + 12);
+            uint32_t e0, e1, e2, e3;
+            if constexpr (kCompact) {
+                e0 = pfc_entry(pf, w[i][0]);
+                e1 = pfc_entry(pf, w[i][1]);
+                e2 = pfc_entry(pf, w[i][2]);
+                e3 = pfc_entry(pf, w[i][3]);
+            } else {
+                uint32_t ad[16];
+                pf_addrs(w[i][0], lb_a, lb_b, ad + 0);
+                pf_addrs(w[i][1], lb_a, lb_b, ad + 4);
+                pf_addrs(w[i][2], lb_a, lb_b, ad + 8);
+                pf_addrs(w[i][3], lb_a, lb_b, ad + 12);
+                e0 = pf_gather(ad + 0);
+                e1 = pf_gather(ad + 4);
+                e2 = pf_gather(ad + 8);
+                e3 = pf_gather(ad + 12);
+            }
             const uint32_t rot = __builtin_amdgcn_mov_dpp(e3, 0x13C, 0xf, 0xf, false);
             const uint32_t ep = lane == 0 ? carry : rot;
             carry = rot;
@@ -709,9 +742,10 @@ __device__ uint32_t g_diag_n;
 // One chain step from chunk start `pos` (< L): an argmax cut (adapters.cpp:59-69), or the tail
 // rule's one or two final cuts (adapters.cpp:48-55), or stop (non-final wait / S7 UB).
 // prm.max_steps == 0 is the raw single next_cut: c1 = the argmax offset, whatever its value.
-__device__ int chain_step(const uint64_t *tl, const uint64_t *th, const TileRecord *rec,
-                          const ChainStream &st, const ChainParams &prm, uint64_t pos,
-                          uint32_t lb_a, uint32_t lb_b, uint64_t &c1, uint64_t &c2) {
+template <bool kCompact>
+__device__ int chain_step(const uint64_t *tl, const uint64_t *th, const uint32_t *pf,
+                          const TileRecord *rec, const ChainStream &st, const ChainParams &prm,
+                          uint64_t pos, uint32_t lb_a, uint32_t lb_b, uint64_t &c1, uint64_t &c2) {
     const uint64_t minl = prm.min_length, maxl = prm.max_length, T = prm.window;
     const bool single = prm.max_steps == 0;
     const uint64_t rem = st.L - pos;
@@ -791,11 +825,11 @@ __device__ int chain_step(const uint64_t *tl, const uint64_t *th, const TileReco
                 const bool m0 = r0.more(), m1 = r1.more();
                 if (!m0 && !m1) break;
                 if (m0) {
-                    r0.compute(w0, lb_a, lb_b, acc_first, acc_last);
+                    r0.template compute<kCompact>(w0, lb_a, lb_b, pf, acc_first, acc_last);
                     if (r0.more()) r0.load(w0);
                 }
                 if (m1) {
-                    r1.compute(w1, lb_a, lb_b, acc_first, acc_last);
+                    r1.template compute<kCompact>(w1, lb_a, lb_b, pf, acc_first, acc_last);
                     if (r1.more()) r1.load(w1);
                 }
             }
@@ -864,9 +898,9 @@ __device__ __forceinline__ uint64_t find_index(const uint64_t *base_arr, uint64_
 // segment i of a longer stream writes its list to the scratch and its count (bit 63 set if the
 // chain ended inside the list: tail rule or stop).
 #ifndef RC_SPEC_WAVES
-#define RC_SPEC_WAVES 16
+#define RC_SPEC_WAVES 4
 #endif
-constexpr int kSpecWaves = RC_SPEC_WAVES;  // walkers per CU when there are enough segments
+constexpr int kSpecWaves = RC_SPEC_WAVES;  // waves per workgroup (20 KiB LDS: ~6 groups per CU)
 
 __global__ __launch_bounds__(kSpecWaves * 64) void rc_spec_kernel(const KeyTables *__restrict__ tab,
                                                       StreamDesc d, uint64_t n_streams,
@@ -876,8 +910,9 @@ __global__ __launch_bounds__(kSpecWaves * 64) void rc_spec_kernel(const KeyTable
                                                       int64_t *__restrict__ counts,
                                                       uint64_t *__restrict__ scratch,
                                                       uint64_t *__restrict__ seg_counts) {
-    stage_tile_tables(tab);
-    const uint64_t *full = reinterpret_cast<const uint64_t *>(s_tile_lds + kFullOff / 4);
+    stage_chain_tables(tab);
+    const uint32_t *pf = s_chain_lds;
+    const uint64_t *full = reinterpret_cast<const uint64_t *>(s_chain_lds + 1024);
     const uint64_t *tl = full, *th = full + 1024;
     const uint32_t lane = lane_id();
     const uint32_t lb_a = (lane & 31) * 4, lb_b = lb_a | 0x10000u;
@@ -911,7 +946,7 @@ __global__ __launch_bounds__(kSpecWaves * 64) void rc_spec_kernel(const KeyTable
         }
         if (!direct && pos >= seg_end && ext++ >= prm.ext_steps) break;
         uint64_t c1 = 0, c2 = 0;
-        const int kind = chain_step(tl, th, rec, st, prm, pos, lb_a, lb_b, c1, c2);
+        const int kind = chain_step<true>(tl, th, pf, rec, st, prm, pos, lb_a, lb_b, c1, c2);
         if (kind == kStepStop) {
             term = true;
             break;
@@ -1092,9 +1127,10 @@ __global__ __launch_bounds__(256) void rc_join_kernel(const KeyTables *__restric
                        __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const bool need = s < n_streams && counts[s] == kNeedJoin;
     if (!__syncthreads_or(need)) return;  // the usual case: nothing to walk in this group
-    stage_tile_tables(tab);
+    stage_chain_tables(tab);
     if (!need) return;
-    const uint64_t *full = reinterpret_cast<const uint64_t *>(s_tile_lds + kFullOff / 4);
+    const uint32_t *pf = s_chain_lds;
+    const uint64_t *full = reinterpret_cast<const uint64_t *>(s_chain_lds + 1024);
     const uint64_t *tl = full, *th = full + 1024;
     const uint32_t lane = lane_id();
     const uint32_t lb_a = (lane & 31) * 4, lb_b = lb_a | 0x10000u;
@@ -1189,7 +1225,7 @@ __global__ __launch_bounds__(256) void rc_join_kernel(const KeyTables *__restric
         }
         if (pos >= st.L) break;
         uint64_t c1 = 0, c2 = 0;
-        const int kind = chain_step(tl, th, rec, st, prm, pos, lb_a, lb_b, c1, c2);
+        const int kind = chain_step<true>(tl, th, pf, rec, st, prm, pos, lb_a, lb_b, c1, c2);
         if (kind == kStepStop) break;
         if (n + (kind == kStepTail2 ? 2 : 1) > cap) {
             overflow = true;

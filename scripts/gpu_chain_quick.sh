@@ -12,6 +12,6 @@ for cfg in 3iii 2 3ii 3iii; do
   tail -n 1 gpurun_out/chainq/bench_$cfg.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('$cfg', d['value'], d['ms_per_step'], r['kernel_ms'], r['chain_kernel_ms'], d['parity_sha256'])"
 done
 for v in ${EDGE_VARIANTS:-}; do
-  RC_LIB_PATH=$PWD/diag/lib_E$v.so timeout -k 10 300 python -u bench.py --config 3iii --steps 5 --warmup 1 --cpu-streams 0 > gpurun_out/chainq/bench_3iii_E$v.log 2>&1 || { echo "bench E$v failed"; exit 5; }
-  tail -n 1 gpurun_out/chainq/bench_3iii_E$v.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('3iii E$v', d['value'], d['ms_per_step'], r['kernel_ms'], r['chain_kernel_ms'], d['parity_sha256'])"
+  RC_LIB_PATH=$PWD/diag/lib_$v.so timeout -k 10 300 python -u bench.py --config 3iii --steps 5 --warmup 1 --cpu-streams 0 > gpurun_out/chainq/bench_3iii_$v.log 2>&1 || { echo "bench E$v failed"; exit 5; }
+  tail -n 1 gpurun_out/chainq/bench_3iii_$v.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('3iii $v', d['value'], d['ms_per_step'], r['kernel_ms'], r['chain_kernel_ms'], d['parity_sha256'])"
 done
