@@ -1360,7 +1360,7 @@ int rc_launch_chain(const KeyTables *d_tables, StreamDesc desc, uint64_t n_strea
                     uint64_t *d_seg_counts, bool any_multi, void *stream) {
     if (n_streams == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
-    // one 144 KiB-LDS workgroup per CU: 4 walkers each, 16 (128 VGPRs) once there are enough
+    // 4-wave workgroups on 20 KiB of LDS (compact tables): about 6 per CU
     const uint64_t wpg = n_segs >= kSpecWaves * (uint64_t)cu_count() ? kSpecWaves : kChainWaves;
     const uint64_t grid = (n_segs + wpg - 1) / wpg;
     hipLaunchKernelGGL(rc_spec_kernel, dim3((unsigned)grid), dim3(wpg * kWaveSize), 0, st,
