@@ -4,14 +4,21 @@ Workload (BASELINE.json configs[1], SURVEY.md §8 d config 2): per GPU, 1024 syn
 splitmix64 streams x 64 MiB (64 GiB resident in HBM), replicat's default chunk parameters
 (min 128,000 / max 5,120,000), unencrypted key (0xff * 16), one piece per stream.
 One step = one pass of the hot path over the whole batch: rc_chunk_device (tile kernel over
-every byte + chain kernel per stream), cut offsets left in HBM.
+every needed byte + chain kernel per stream), cut offsets left in HBM.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3i|3ii|3iii|4|5|harness]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (N > 1)
 
-Ranks shard the work per stream (stream ids rank*1024 ..), with no data-path collective:
-"scaling": "weak".  Rank 0 prints one JSON line.  Parity is checked in-run: rank 0's cut lists
-hash to the reference's SHA-256 for config 2 (tests/golden/digests.json).
+Ranks shard the work per stream (config 2: stream ids rank*1024 ..; config 4: stream i on
+GPU i mod 8) with no data-path collective: "scaling": "weak".  The process group is gloo and
+carries only the barriers, the max-over-ranks time and the parity flags -- never stream data.
+Rank 0 prints one JSON line.  Parity is checked in-run against the reference's cut-list
+digests (tests/golden: config 2, 3 (ii), 3 (iii), 4 on every rank, 5, harness).
+
+`--config harness` is the reference's own benchmark (Repository._benchmark_chunker,
+/root/reference/replicat/repository.py:1984-2008): 10 x 512,000,000 Random(0) bytes as one
+stream of 10 pieces, here chunked on the device in one call; its cpu_baseline is that harness
+itself -- the reference's native chunker (oracle/_ref) under replicat's adapter loop.
 """
 import argparse
 import json
@@ -28,129 +35,135 @@ GIB = 1 << 30
 MIN_LEN, MAX_LEN = 128_000, 5_120_000
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
 
+# name -> (streams per GPU, MiB per stream, min_length, max_length)
+CONFIGS = {'2': (1024, 64, MIN_LEN, MAX_LEN), '3i': (65536, 1, MIN_LEN, MAX_LEN),
+           '3ii': (1, 64 << 10, MIN_LEN, MAX_LEN), '3iii': (65536, 1, 2_000, 80_000),
+           '4': (16, 8192, MIN_LEN, MAX_LEN), '5': (1024, 64, MIN_LEN, MAX_LEN),
+           'harness': (1, 0, MIN_LEN, MAX_LEN)}
 
-def parse():
+
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument('--gpus', type=int, default=1)
     p.add_argument('--steps', type=int, default=10)
     p.add_argument('--warmup', type=int, default=2)
-    p.add_argument('--config', choices=['2', '3i', '3ii', '3iii', '4', '5'], default='2',
+    p.add_argument('--config', choices=sorted(CONFIGS), default='2',
                    help='2: 1024 x 64 MiB (the metric); 3i: 65536 x 1 MiB default params '
                         '(degenerate: tail rule only); 3ii: ONE 64 GiB stream, last piece the '
                         'final 1 MiB (snapshot framing, segment-parallel chain); 3iii: 65536 x '
                         '1 MiB, min 2000 / max 80000; 4: 16 x 8 GiB per GPU (streams rank, '
                         'rank+8, ...); 5: re-chunk of config 2 with 512 edited copies + dedup '
-                        'ratio check')
+                        'ratio check; harness: the reference benchmark stream (10 x 512 MB)')
     p.add_argument('--streams', type=int, default=None)
     p.add_argument('--stream-mib', type=int, default=None)
     p.add_argument('--calibrate', action='store_true',
                    help='also time a pure streaming read of the same bytes (rc_read_probe)')
     p.add_argument('--key', choices=['ff', 'seeded'], default='ff')
-    p.add_argument('--cpu-streams', type=int, default=256,
-                   help='bounded CPU-baseline sample (64 MiB streams); 0 = skip')
-    p.add_argument('--cpu-procs', type=int, default=16)
+    p.add_argument('--cpu-streams', type=int, default=None,
+                   help='CPU-baseline sample in streams (default: all of config 2); 0 = skip')
+    p.add_argument('--cpu-procs', type=int, default=None,
+                   help='CPU-baseline processes (default: the cores this process may use)')
     p.add_argument('--e2e', action='store_true', help='also time the host-resident path')
     p.add_argument('--no-verify', action='store_true')
-    return p.parse_args()
+    return p.parse_args(argv)
 
 
-def cut_digest(cuts_dev, counts_dev, caps):
-    sys.path.insert(0, os.path.join(ROOT, 'tests'))
-    import golden_util as G
-    cuts = cuts_dev.cpu().numpy().view(np.uint64)
-    counts = counts_dev.cpu().numpy()
-    base = np.concatenate([[0], np.cumsum(caps)[:-1]]).astype(np.int64)
-    ends = [cuts[b:b + c] for b, c in zip(base, counts)]
-    return G.cutlist_digest(ends), int(counts.sum()), ends
+# ------------------------------------------------------------------ device plumbing
+
+class Backend:
+    """Everything bench.py does on a GPU: device selection, memory, synthetic fills, the chunker.
+    tests/test_bench_ranks.py substitutes a CPU stand-in to run main() under gloo ranks."""
+
+    device = 'cuda'
+
+    def __init__(self, local_rank):
+        import torch
+        self.torch = torch
+        self.index = local_rank
+        torch.cuda.set_device(local_rank)
+
+    def empty(self, nbytes):
+        return self.torch.empty(nbytes, dtype=self.torch.uint8, device=self.device)
+
+    def zeros_i64(self, n):
+        return self.torch.zeros(max(n, 1), dtype=self.torch.int64, device=self.device)
+
+    def stream(self):
+        return self.torch.cuda.current_stream().cuda_stream
+
+    def synchronize(self):
+        self.torch.cuda.synchronize()
+
+    def chunker(self, min_len, max_len, key):
+        from replicat_amd.chunker import GpuChunker
+        return GpuChunker(min_len, max_len, key, device=self.index)
+
+    def fill_streams(self, ptr, n, size, slot, seed, first_id, id_step):
+        from replicat_amd.chunker import fill_splitmix_streams
+        fill_splitmix_streams(ptr, n, size, slot, seed, first_id, id_step, self.stream())
+
+    def fill_at(self, ptr, nbytes, seed, stream_id, word0):
+        from replicat_amd.chunker import fill_splitmix_at
+        fill_splitmix_at(ptr, nbytes, seed, stream_id, word0, self.stream())
+
+    def upload(self, dst_tensor, host_bytes):
+        dst_tensor[:len(host_bytes)].copy_(self.torch.frombuffer(host_bytes, dtype=self.torch.uint8))
+
+    def read_probe_gbs(self, ptr, nbytes):
+        from replicat_amd.chunker import read_probe
+        torch = self.torch
+        out = torch.zeros(4, dtype=torch.int32, device=self.device)
+        st = torch.cuda.current_stream()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        probe = nbytes // 16 * 16
+        for _ in range(2):
+            read_probe(ptr, probe, out.data_ptr(), self.stream())
+        ev0.record(st)
+        for _ in range(5):
+            read_probe(ptr, probe, out.data_ptr(), self.stream())
+        ev1.record(st)
+        torch.cuda.synchronize()
+        return round(5 * probe / (ev0.elapsed_time(ev1) * 1e-3) / 1e9, 1)
 
 
-# ------------------------------------------------------------------------ CPU baseline
+class Ranks:
+    """The process group of a multi-GPU run: gloo (host) only.  The data path has no exchange;
+    this carries the start/stop barriers, the max-over-ranks time and small host objects."""
 
-def _cpu_worker(args):
-    kind, ids, size, seed = args
-    from replicat_amd import synth
-    out = []
-    if kind == 'reference':
-        sys.path.insert(0, os.path.join(ROOT, 'oracle', '_ref'))
-        import _replicat_adapters as ref  # the reference's own chunker, built by oracle/Makefile
-        ch = ref._gclmulchunker(MIN_LEN, MAX_LEN, b'\xff' * 16)
-        t = 0.0
-        for i in ids:
-            data = synth.stream_bytes(size, seed, i)
-            mv = memoryview(data)
-            t0 = time.perf_counter()
-            pos, ends = 0, []
-            while pos < size:  # next_cut on a zero-copy view: the native scan alone
-                c = ch.next_cut(mv[pos:], True)
-                if not c:
-                    break
-                pos += c
-                ends.append(pos)
-            t += time.perf_counter() - t0
-            out.append(ends)
-        return t, out
-    from oracle import oracle as o
-    t = 0.0
-    for i in ids:
-        data = synth.stream_bytes(size, seed, i)
-        t0 = time.perf_counter()
-        out.append(o.chunk_stream(data, MIN_LEN, MAX_LEN, None, 0))
-        t += time.perf_counter() - t0
-    return t, out
+    def __init__(self):
+        self.world = int(os.environ.get('WORLD_SIZE', '1'))
+        self.rank = int(os.environ.get('RANK', '0'))
+        self.local = int(os.environ.get('LOCAL_RANK', str(self.rank)))
+        self.dist = None
+        if self.world > 1:
+            import torch.distributed as dist
+            if not dist.is_initialized():
+                dist.init_process_group('gloo')
+            self.dist = dist
 
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
 
-def cpu_baseline(n_streams, size, seed, procs):
-    import multiprocessing as mp
-    import glob
-    kind = 'reference' if glob.glob(os.path.join(ROOT, 'oracle', '_ref', '_replicat_adapters*.so')) \
-        else 'port'
-    if kind == 'port':
-        from oracle import oracle as o
-        o.lib()
-    procs = max(1, min(procs, n_streams))
-    shards = [list(range(r, n_streams, procs)) for r in range(procs)]
-    t0 = time.perf_counter()
-    with mp.get_context('fork').Pool(procs) as pool:
-        res = pool.map(_cpu_worker, [(kind, s, size, seed) for s in shards])
-    wall = time.perf_counter() - t0
-    busiest = max(r[0] for r in res)  # scan time of the slowest process (generation excluded)
-    ends = {}
-    for s, (_, out) in zip(shards, res):
-        for i, e in zip(s, out):
-            ends[i] = e
-    gibs = n_streams * size / busiest / GIB
-    return {'value': round(gibs, 3), 'unit': 'GiB/s', 'cores': procs, 'kind': kind,
-            'sample': f'{n_streams} x {size >> 20} MiB of the same synthetic streams '
-                      f'(ids 0..{n_streams - 1}), one process per core, '
-                      f'native next_cut scan time of the slowest process ({busiest:.2f} s; '
-                      f'{wall:.1f} s wall incl. data generation)'}, ends
+    def max(self, values):
+        if not self.dist:
+            return list(values)
+        import torch
+        t = torch.tensor(values, dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return t.tolist()
 
+    def gather(self, obj):
+        if not self.dist:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
 
-# ---------------------------------------------------------------- PMC traffic (profiles/)
+    def close(self):
+        if self.dist and self.dist.is_initialized():
+            self.dist.destroy_process_group()
 
-def pmc_traffic(args, n, size):
-    """HBM bytes per rc_tile_kernel launch from the committed rocprofv3 PMC summary of this same
-    command (scripts/gpu_profile.sh -> scripts/summarize_profile.py: separate --pmc passes,
-    FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM, WRITE_SIZE as is), or None when no summary
-    covers this workload.  bench.py cannot read counters itself (that needs rocprofv3)."""
-    if not (args.config == '2' and args.key == 'ff' and n == 1024 and size == 64 << 20):
-        return None, None
-    import glob
-    for f in sorted(glob.glob(os.path.join(ROOT, 'profiles', 'r*', 'pmc_summary.json')),
-                    reverse=True):
-        try:
-            with open(f) as fh:
-                d = json.load(fh)
-        except (OSError, ValueError):
-            continue
-        t = d.get('rc_tile_kernel', {})
-        if d.get('workload') == 'config2' and 'hbm_read_bytes_corrected' in t:
-            return (t['hbm_read_bytes_corrected'] + t.get('hbm_write_bytes', 0.0),
-                    os.path.relpath(f, ROOT))
-    return None, None
-
-
-# ------------------------------------------------------------------- multi-GPU plumbing
 
 def shard_ids(config, rank, n):
     """Stream ids a rank chunks (weak scaling: every rank has its own n streams).  Config 4
@@ -161,12 +174,196 @@ def shard_ids(config, rank, n):
 
 
 def reduce_max(values, dist, device):
-    """Max over ranks of a few floats (elapsed time, kernel times): the job is as slow as its
-    slowest rank.  The only collective the bench uses besides its barriers."""
+    """Max over ranks of a few floats through an initialised process group (kept for callers
+    that hold their own group; main() uses Ranks.max)."""
     import torch
     t = torch.tensor(values, dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return t.tolist()
+
+
+def cut_digest(cuts_dev, counts_dev, caps):
+    sys.path.insert(0, os.path.join(ROOT, 'tests'))
+    import golden_util as G
+    cuts = cuts_dev.cpu().numpy().view(np.uint64)
+    counts = counts_dev.cpu().numpy()[:len(caps)]
+    base = np.concatenate([[0], np.cumsum(caps)[:-1]]).astype(np.int64)
+    ends = [cuts[b:b + c] for b, c in zip(base, counts)]
+    return G.cutlist_digest(ends), int(counts.sum()), ends
+
+
+def bytes_needed(max_length, lens, last):
+    """Bytes the tile kernel must read: per stream, bytes [0, 4 jneed + 4) with jneed the last
+    key any argmax window reaches (rc_keys_needed; 0 = tail rule only, nothing read)."""
+    from replicat_amd.chunker import keys_needed
+    memo, total = {}, 0
+    for L, P in zip(lens, last if last is not None else [0] * len(lens)):
+        k = (int(L), int(P))
+        if k not in memo:
+            j = keys_needed(max_length, k[0], k[1])
+            memo[k] = min(k[0], 4 * j + 4) if j else 0
+        total += memo[k]
+    return total
+
+
+# ------------------------------------------------------------------------ CPU baseline
+
+def cpu_share():
+    """(cores to use, cores in the affinity mask): the mask, capped by the CPU share the GPU box
+    grants one GPU (OMP_NUM_THREADS there; nproc and the mask show the whole machine)."""
+    n = len(os.sched_getaffinity(0))
+    cap = os.environ.get('OMP_NUM_THREADS')
+    if cap and cap.isdigit() and int(cap) > 0:
+        return min(n, int(cap)), n
+    return n, n
+
+
+def _ref_chunker(min_len, max_len, key):
+    """The reference's own chunker, compiled from /root/reference/src/adapters.cpp into
+    oracle/_ref by oracle/Makefile (built in the build container, shipped with the tree)."""
+    import glob
+    import importlib.machinery
+    import importlib.util
+    so = glob.glob(os.path.join(ROOT, 'oracle', '_ref', '_replicat_adapters*.so'))
+    if not so:
+        return None
+    loader = importlib.machinery.ExtensionFileLoader('_replicat_adapters', so[0])
+    spec = importlib.util.spec_from_loader('_replicat_adapters', loader)
+    mod = importlib.util.module_from_spec(spec)
+    loader.exec_module(mod)
+    return mod._gclmulchunker(min_len, max_len, key)
+
+
+def _stream(size, seed, sid):
+    from oracle import oracle as o
+    return o.fill_splitmix(size, seed, sid)
+
+
+def _scan_worker(args):
+    """Native next_cut scan (the reference's, else the oracle port) over whole streams, on a
+    zero-copy view: exactly the adapter's calls for a single piece (adapters.py:290-305)."""
+    kind, ids, size, seed, min_len, max_len = args
+    from oracle import oracle as o
+    ref = _ref_chunker(min_len, max_len, b'\xff' * 16) if kind == 'reference' else None
+    t, out = 0.0, []
+    for i in ids:
+        data = _stream(size, seed, i)
+        t0 = time.perf_counter()
+        if ref is not None:
+            mv, pos, ends = memoryview(data), 0, []
+            while pos < size:
+                c = ref.next_cut(mv[pos:], True)
+                if not c:
+                    break
+                pos += c
+                ends.append(pos)
+        else:
+            ends = o.chunk_stream(data, min_len, max_len, None, 0)
+        t += time.perf_counter() - t0
+        out.append((i, ends))
+    return t, out
+
+
+def _adapter_worker(args):
+    """replicat's adapter loop (oracle/adapter_loop.py) over the reference's native chunker,
+    fed 16 MiB pieces as Repository.snapshot reads files (repository.py:1413,1440)."""
+    ids, size, seed, min_len, max_len = args
+    from oracle.adapter_loop import adapter_chunks
+    t = 0.0
+    for i in ids:
+        data = _stream(size, seed, i)
+        pieces = [data[k:k + (16 << 20)].tobytes() for k in range(0, size, 16 << 20)]
+        ref = _ref_chunker(min_len, max_len, b'\xff' * 16)
+        t0 = time.perf_counter()
+        n = sum(len(c) for c in adapter_chunks(ref, pieces))
+        t += time.perf_counter() - t0
+        assert n == size
+    return t
+
+
+def _pool_map(fn, jobs):
+    import multiprocessing as mp
+    with mp.get_context('fork').Pool(len(jobs)) as pool:
+        return pool.map(fn, jobs)
+
+
+def cpu_baseline(n_streams, size, seed, procs, min_len=MIN_LEN, max_len=MAX_LEN):
+    """the reference's native scan on the box's host cores, one process per
+    core, over `n_streams` of the same synthetic streams; the adapter-loop rate beside it; and
+    the speed ratio of the reference build to the oracle port on the same sample."""
+    import glob
+    from oracle import oracle as o
+    o.lib()
+    kind = 'reference' if glob.glob(os.path.join(ROOT, 'oracle', '_ref', '_replicat_adapters*.so')) \
+        else 'port'
+    procs = max(1, min(procs, n_streams))
+    shards = [list(range(r, n_streams, procs)) for r in range(procs)]
+    t0 = time.perf_counter()
+    res = _pool_map(_scan_worker, [(kind, s, size, seed, min_len, max_len) for s in shards])
+    wall = time.perf_counter() - t0
+    busiest = max(r[0] for r in res)  # scan time of the slowest process (generation excluded)
+    ends = {i: e for _, out in res for i, e in out}
+    out = {'value': round(n_streams * size / busiest / GIB, 3), 'unit': 'GiB/s', 'cores': procs,
+           'kind': kind,
+           'sample': f'{n_streams} x {size >> 20} MiB of the same synthetic streams (ids '
+                     f'0..{n_streams - 1}), one process per core, native next_cut scan time of '
+                     f'the slowest process ({busiest:.2f} s; {wall:.1f} s wall incl. data '
+                     f'generation)'}
+    if kind == 'reference':
+        # the adapter loop: one stream per core (16 MiB pieces), and the reference-vs-port
+        # time ratio on two streams in this process
+        k = min(procs, n_streams)
+        ta = max(_pool_map(_adapter_worker, [([i], size, seed, min_len, max_len) for i in range(k)]))
+        out['adapter_loop'] = {'value': round(k * size / ta / GIB, 3), 'unit': 'GiB/s',
+                               'cores': k, 'sample': f'{k} x {size >> 20} MiB in 16 MiB pieces '
+                               f'through adapters.py:290-305 (restated, oracle/adapter_loop.py)'}
+        tr, _ = _scan_worker(('reference', [0, 1], size, seed, min_len, max_len))
+        tp, _ = _scan_worker(('port', [0, 1], size, seed, min_len, max_len))
+        out['reference_time_over_port_time'] = round(tr / tp, 3)
+    return out, ends
+
+
+def harness_cpu(pieces, min_len, max_len):
+    """The reference harness itself on one host core: its native chunker under replicat's adapter
+    loop over the 10 pre-built pieces (generation outside the clock, as repository.py:2001-2003)."""
+    from oracle.adapter_loop import harness_rate
+    ref = _ref_chunker(min_len, max_len, b'\xff' * 16)
+    if ref is None:
+        return None, None
+    nbytes, secs, lengths = harness_rate(ref, pieces)
+    return ({'value': round(nbytes / secs / GIB, 3), 'unit': 'GiB/s', 'cores': 1,
+             'kind': 'reference', 'rate_GBps': round(nbytes / secs / 1e9, 3),
+             'sample': f'the whole harness stream ({nbytes} B, 10 pieces) through the adapter '
+                       f'loop, {secs:.2f} s, generation excluded (repository.py:1984-2008)'},
+            lengths)
+
+
+# ---------------------------------------------------------------- PMC traffic (profiles/)
+
+def pmc_traffic(config, n, size, build_id):
+    """HBM bytes per rc_tile_kernel launch from the committed rocprofv3 PMC summary of this same
+    command (scripts/gpu_profile.sh -> scripts/summarize_profile.py: separate --pmc passes,
+    FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM, WRITE_SIZE as is).  Only a summary of the
+    SAME library build counts: it is stamped with rc_build_id(), and a stale one is refused.
+    bench.py cannot read counters itself (that needs rocprofv3)."""
+    if not (config == '2' and n == 1024 and size == 64 << 20):
+        return None, 'no PMC summary for this workload'
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, 'profiles', 'r*', 'pmc_summary.json')),
+                    reverse=True):
+        try:
+            with open(f) as fh:
+                d = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        t = d.get('rc_tile_kernel', {})
+        if d.get('workload') != 'config2' or 'hbm_read_bytes_corrected' not in t:
+            continue
+        if d.get('build_id') != build_id:
+            return None, f'{os.path.relpath(f, ROOT)} is of build {d.get("build_id")}, not {build_id}'
+        return (t['hbm_read_bytes_corrected'] + t.get('hbm_write_bytes', 0.0),
+                os.path.relpath(f, ROOT))
+    return None, 'no PMC summary under profiles/'
 
 
 # ------------------------------------------------------------------- config 5 (dedup)
@@ -182,7 +379,7 @@ class Config5:
     up by BLAKE2b-512 content digest over the whole original set instead, so the two agree only
     if no other coincidence exists."""
 
-    def __init__(self, ch, pool, slot, n, size, rank, hs):
+    def __init__(self, ch, pool, slot, n, size, rank, hs, device='cuda'):
         import torch
         from replicat_amd import synth
         self.size, self.slot, self.n = size, slot, n
@@ -190,15 +387,15 @@ class Config5:
         base = pool.data_ptr()
         olens = [size] * n
         cap, ocaps = ch.capacity(olens)
-        ocuts = torch.zeros(cap, dtype=torch.int64, device='cuda')
-        ocounts = torch.zeros(n, dtype=torch.int64, device='cuda')
+        ocuts = torch.zeros(cap, dtype=torch.int64, device=device)
+        ocounts = torch.zeros(n, dtype=torch.int64, device=device)
         ch.chunk_device([base + i * slot for i in range(n)], olens, None, ocuts.data_ptr(),
                         ocounts.data_ptr(), hs)
         self.orig_digest, _, self.orig_ends = cut_digest(ocuts, ocounts, ocaps)
         plan = synth.edit_plan(n, n // 2, size) if rank == 0 and n == 1024 else []
         self.plan = {sid: (kind, off, payload) for sid, kind, off, payload in plan}
         self.edited = sorted(self.plan)
-        self.buf = torch.empty(n * slot + 64, dtype=torch.uint8, device='cuda')
+        self.buf = torch.empty(n * slot + 64, dtype=torch.uint8, device=device)
         self.lens = []
         for i in range(n):
             src = pool[i * slot:i * slot + size]
@@ -258,108 +455,170 @@ class Config3ii:
     speculative chain, the ranks exchange their cut lists through a host-side (gloo) gather and
     splice them.  One rank: the plain single-stream path (segment-parallel chain on one GPU)."""
 
-    def __init__(self, ch, size, rank, world, hs, dist):
-        import torch
+    def __init__(self, ch, size, ranks, be):
         from replicat_amd import split, synth
-        from replicat_amd.chunker import fill_splitmix_at
-        self.ch, self.rank, self.world, self.hs = ch, rank, world, hs
-        self.L = size * world
+        self.ch, self.ranks, self.be = ch, ranks, be
+        self.rank, self.world = ranks.rank, ranks.world
+        self.hs = be.stream()
+        self.L = size * self.world
         self.P = self.L - (1 << 20)
-        self.windows = split.plan_windows(self.L, self.P, world, ch.max_length)
-        w = self.windows[rank]
+        self.windows = split.plan_windows(self.L, self.P, self.world, ch.max_length)
+        w = self.windows[self.rank]
         self.w = w
-        self.buf = torch.empty(w.end - w.start + 64, dtype=torch.uint8, device='cuda')
-        fill_splitmix_at(self.buf.data_ptr(), w.end - w.start, synth.DEFAULT_SEED, 0,
-                         w.start // 8, hs)
+        self.buf = be.empty(w.end - w.start + 64)
+        be.fill_at(self.buf.data_ptr(), w.end - w.start, synth.DEFAULT_SEED, 0, w.start // 8)
         self.lens = [w.end - w.start]
         _, caps = ch.capacity(self.lens)
         self.cap = int(caps[0])
-        self.cuts = torch.zeros(self.cap + 1, dtype=torch.int64, device='cuda')
-        self.counts = torch.zeros(1, dtype=torch.int64, device='cuda')
-        self.group = dist.new_group(backend='gloo') if world > 1 else None
-        self.dist = dist
+        self.cuts = be.zeros_i64(self.cap + 1)
+        self.counts = be.zeros_i64(1)
         self.ends = None
         self.rounds = 0
 
     def chunk_window(self, w, entry):
-        import torch
         off = entry - w.start
         src, n = self.buf.data_ptr() + off, w.end - entry
         tmp = None
         if src % 16:  # a fallback entry (rare): re-base the bytes on an aligned buffer
-            tmp = torch.empty(n + 64, dtype=torch.uint8, device='cuda')
+            tmp = self.be.empty(n + 64)
             tmp[:n].copy_(self.buf[off:off + n])
             src = tmp.data_ptr()
         _, caps = self.ch.capacity([n])
-        cuts = self.cuts if int(caps[0]) <= self.cap else \
-            torch.zeros(int(caps[0]), dtype=torch.int64, device='cuda')
+        cuts = self.cuts if int(caps[0]) <= self.cap else self.be.zeros_i64(int(caps[0]))
         self.ch.chunk_device([src], [n], [max(0, w.last_piece - off) if not w.open else 0],
                              cuts.data_ptr(), self.counts.data_ptr(), self.hs, open_=w.open)
-        c = int(self.counts.item())
+        c = int(self.counts.cpu()[0])
         return (cuts[:c].cpu().numpy() + entry).tolist()
-
-    def gather(self, obj):
-        if self.world == 1:
-            return [obj]
-        out = [None] * self.world
-        self.dist.all_gather_object(out, obj, group=self.group)
-        return out
 
     def step(self):
         from replicat_amd import split
         self.ends, self.rounds = split.chunk_split(self.chunk_window, self.windows, self.rank,
-                                                   self.gather)
+                                                   self.ranks.gather)
 
 
 # ------------------------------------------------------------------------------ main
 
-def main():
-    args = parse()
-    import torch
-    import torch.distributed as dist
+def _golden():
+    sys.path.insert(0, os.path.join(ROOT, 'tests'))
+    import golden_util as G
+    return G
 
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
-    torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+
+def check_parity(args, n, size, rank, long, edit, ends, digest):
+    """(flag, scope) of this rank's cut lists against the reference's digests, or (None, None)
+    when no fixture covers the workload."""
+    G = _golden()
+    gold = {d['name']: d for d in G.load('digests.json')}
+    ff = args.key == 'ff'
+    if args.config == '2' and ff and n == 1024 and size == 64 << 20 and rank == 0:
+        return digest == gold['config2_ff']['sha256'], 'rank 0 (streams 0..1023)'
+    if args.config == '3iii' and ff and rank == 0 and n == 65536:
+        return digest == gold['config3iii']['sha256'], 'all 65536 streams'
+    if args.config == '3iii' and ff and rank == 0 and n >= 4096:
+        return (G.cutlist_digest(ends[:4096]) == gold['config3iii_first4096']['sha256'],
+                'first 4096 streams')
+    if args.config == '3i' and ff and rank == 0:
+        # the tail rule alone: one chunk per stream (adapters.cpp:50-51)
+        return all(len(e) == 1 and int(e[0]) == size for e in ends), 'every stream'
+    if long is not None and ff and long.L == 64 << 30:
+        large = {d['name']: d for d in G.load('large.json')}
+        return digest == large['config3ii']['sha256'], 'the whole stream'
+    if args.config == '4' and ff and n == 16 and size == 8 << 30 and rank < 8:
+        c4 = G.load('config4.json')
+        return digest == c4['per_gpu'][rank]['sha256'], 'every rank: streams r, r + 8, ..'
+    if args.config == 'harness':
+        return digest == G.load('harness.json')['sha256'], 'the whole harness stream'
+    if edit is not None and ff and n == 1024 and size == 64 << 20 and rank == 0:
+        large = {d['name']: d for d in G.load('large.json')}
+        dedup = edit.result = edit.dedup(ends)
+        g5 = large['config5']
+        return ((G.cutlist_digest([ends[i] for i in edit.edited]) == g5['edited_sha256']
+                 and edit.orig_digest == g5['original_sha256']
+                 and dedup['dup_bytes_edited'] == g5['dup_bytes_edited']
+                 and dedup['total_bytes_edited'] == g5['total_bytes_edited']),
+                'rank 0 (512 edited streams + dedup)')
+    return None, None
+
+
+def roofline(bytes_per_step, read, tile_avg, edge_avg, chain_avg, traffic, traffic_src, bid):
+    """The tile kernel against the HBM read peak, on two bases: the stream bytes a launch
+    covers (SURVEY §8 d's algorithmic bytes) and the bytes it must read (up to each stream's
+    last needed key -- the tail rule's last ~max_length bytes are never read).  Null when the
+    kernel reads nothing or the figure would pass the peak (then it is not a measurement)."""
+    r = {'bound': 'hbm', 'kernel': 'rc_tile_kernel', 'unit': 'GB/s', 'peak': HBM_PEAK_GBS,
+         'kernel_ms': round(tile_avg, 3), 'edge_kernel_ms': round(edge_avg, 3),
+         'chain_kernel_ms': round(chain_avg, 3), 'algorithmic_bytes': bytes_per_step,
+         'bytes_read': read, 'traffic': None if traffic is None else round(traffic),
+         'traffic_source': traffic_src, 'build_id': bid,
+         'basis': 'stream bytes per tile-kernel launch (SURVEY §8 d)',
+         'basis_read': "bytes the tile kernel must read (to each stream's last needed key)"}
+    ok = read > 0 and tile_avg > 0
+    achieved = bytes_per_step / (tile_avg * 1e-3) / 1e9 if ok else None
+    achieved_read = read / (tile_avg * 1e-3) / 1e9 if ok else None
+    if ok and achieved_read > HBM_PEAK_GBS:
+        ok = False
+    r.update({'achieved': round(achieved, 1) if ok else None,
+              'frac': round(achieved / HBM_PEAK_GBS, 4) if ok else None,
+              'achieved_read': round(achieved_read, 1) if ok else None,
+              'frac_read': round(achieved_read / HBM_PEAK_GBS, 4) if ok else None})
+    if not ok:
+        r['note'] = ('no key is hashed: every stream is cut by the tail rule alone '
+                     '(adapters.cpp:48-55); no roofline') if read == 0 else 'not a measurement'
+    return r
+
+
+def main(argv=None, backend=Backend):
+    args = parse(argv)
+    ranks = Ranks()
+    world, rank = ranks.world, ranks.rank
+    be = backend(ranks.local)
 
     from replicat_amd import synth
-    from replicat_amd.chunker import GpuChunker, fill_splitmix, read_probe
     key = b'\xff' * 16 if args.key == 'ff' else synth.seeded_key(1)
-    cfg = {'2': (1024, 64, MIN_LEN, MAX_LEN), '3i': (65536, 1, MIN_LEN, MAX_LEN),
-           '3ii': (1, 64 << 10, MIN_LEN, MAX_LEN), '3iii': (65536, 1, 2_000, 80_000),
-           '4': (16, 8192, MIN_LEN, MAX_LEN), '5': (1024, 64, MIN_LEN, MAX_LEN)}[args.config]
+    cfg = CONFIGS[args.config]
     n = args.streams or cfg[0]
     size = (args.stream_mib or cfg[1]) << 20
     min_len, max_len = cfg[2], cfg[3]
-    ch = GpuChunker(min_len, max_len, key, device=local)
-    stream = torch.cuda.current_stream()
-    hs = stream.cuda_stream
+    ch = be.chunker(min_len, max_len, key)
+    hs = be.stream()
     last = None
-    edit = long = None
+    edit = long = harness = None
     if args.config == '3ii':
-        long = Config3ii(ch, size, rank, world, hs, dist)
+        long = Config3ii(ch, size, ranks, be)
         n, lens = 1, long.lens
         base_ptr = long.buf.data_ptr()
+        last = [long.w.last_piece if not long.w.open else 0]
+    elif args.config == 'harness':
+        # the reference benchmark's stream, generated on the host as the reference does, copied
+        # in once; the timed step chunks it on the device
+        harness = list(synth.harness_buffers())
+        L = sum(len(b) for b in harness)
+        pool = be.empty(L + 64)
+        off = 0
+        for b in harness:
+            be.upload(pool[off:], b)
+            off += len(b)
+        n, size, lens, last = 1, L, [L], [L - len(harness[-1])]
+        base_ptr = pool.data_ptr()
+        ptrs = [base_ptr]
     else:
         # stream slots 64-B aligned; config 5's inserts grow a stream by up to 4 bytes
         slot = (size + (64 if args.config == '5' else 0) + 63) // 64 * 64
-        pool = torch.empty(n * slot + 64, dtype=torch.uint8, device='cuda')  # one arena
+        pool = be.empty(n * slot + 64)  # one arena
         base_ptr = pool.data_ptr()
         ptrs = [base_ptr + i * slot for i in range(n)]
-        for p, i in zip(ptrs, shard_ids(args.config, rank, n)):
-            fill_splitmix(p, size, synth.DEFAULT_SEED, i, hs)
+        ids = shard_ids(args.config, rank, n)
+        be.fill_streams(base_ptr, n, size, slot, synth.DEFAULT_SEED, ids[0],
+                        ids[1] - ids[0] if n > 1 else 1)
         lens = [size] * n
         if args.config == '5':
             # the original set is chunked once (untimed); the step re-chunks the edited set
-            edit = Config5(ch, pool, slot, n, size, rank, hs)
+            edit = Config5(ch, pool, slot, n, size, rank, hs, be.device)
             ptrs, lens = edit.ptrs, edit.lens
     total_cap, caps = ch.capacity(lens)
-    cuts = torch.zeros(total_cap, dtype=torch.int64, device='cuda')
-    counts = torch.zeros(n, dtype=torch.int64, device='cuda')
-    torch.cuda.synchronize()
+    cuts = be.zeros_i64(total_cap)
+    counts = be.zeros_i64(n)
+    be.synchronize()
 
     def step():
         if long is not None:
@@ -369,109 +628,62 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+    be.synchronize()
+    ranks.barrier()
+    be.synchronize()
     ch.timing(True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+    be.synchronize()
+    ranks.barrier()
+    be.synchronize()
     elapsed = time.perf_counter() - t0
     ch.timing(False)
-    a_ms, b_ms, calls = ch.read_timing()
-    if world > 1:
-        elapsed, a_ms, b_ms = reduce_max([elapsed, a_ms, b_ms], dist, 'cuda')
+    tile_ms, edge_ms, chain_ms, calls = ch.read_kernel_timing()
+    elapsed, tile_ms, edge_ms, chain_ms = ranks.max([elapsed, tile_ms, edge_ms, chain_ms])
 
     bytes_per_step = sum(lens) if long is None else long.L // world
     value = world * bytes_per_step * args.steps / elapsed / GIB
     ms_per_step = elapsed * 1e3 / args.steps
-    a_avg = a_ms / max(calls, 1)
-    b_avg = b_ms / max(calls, 1)
-    achieved = bytes_per_step / (a_avg * 1e-3) / 1e9  # GB/s, ΣL per tile-kernel launch
+    calls = max(calls, 1)
 
-    parity = None
-    ends = None
-    if not args.no_verify and rank == 0:
-        sys.path.insert(0, os.path.join(ROOT, 'tests'))
-        import golden_util as G
+    parity, ends, scope = None, None, None
+    if not args.no_verify:
         if long is not None:
             ends = [np.asarray(long.ends, dtype=np.uint64)]
-            digest = G.cutlist_digest(ends)
+            digest = _golden().cutlist_digest(ends)
         else:
-            digest, nchunks, ends = cut_digest(cuts, counts, caps)
-        gold = {d['name']: d for d in G.load('digests.json')}
-        if args.key == 'ff' and n == 1024 and size == 64 << 20 and args.config == '2':
-            parity = digest == gold['config2_ff']['sha256']
-        elif args.key == 'ff' and args.config == '3iii' and n >= 4096:
-            parity = G.cutlist_digest(ends[:4096]) == gold['config3iii_first4096']['sha256']
-        elif args.key == 'ff' and long is not None and long.L == 64 << 30:
-            large = {d['name']: d for d in G.load('large.json')}
-            parity = digest == large['config3ii']['sha256']
-        elif edit is not None and args.key == 'ff' and n == 1024 and size == 64 << 20:
-            large = {d['name']: d for d in G.load('large.json')}
-            dedup = edit.result = edit.dedup(ends)
-            g5 = large['config5']
-            parity = (G.cutlist_digest([ends[i] for i in edit.edited]) == g5['edited_sha256']
-                      and edit.orig_digest == g5['original_sha256']
-                      and dedup['dup_bytes_edited'] == g5['dup_bytes_edited']
-                      and dedup['total_bytes_edited'] == g5['total_bytes_edited'])
-    if world > 1:
-        dist.barrier()
+            digest, _, ends = cut_digest(cuts, counts, caps)
+        parity, scope = check_parity(args, n, size, rank, long, edit, ends, digest)
+    flags = ranks.gather(parity)
+    if args.config == '4' and all(f is not None for f in flags):
+        parity = all(flags)  # every rank checked its own shard
+        scope = f'{len(flags)} rank(s), each its own 16 streams'
 
-    if long is not None:
-        workload = ('config3ii: ONE stream of %d GiB (last piece = final 1 MiB) split over %d '
-                    'rank(s), min %d, max %d, key %s' % (long.L >> 30, world, min_len, max_len,
-                                                         args.key))
-    else:
-        workload = ('config%s: %d x %d MiB streams per GPU, min %d, max %d, key %s'
-                    % (args.config, n, size >> 20, min_len, max_len, args.key))
-        if edit is not None:
-            workload += ' (512 of the 1024 edited, re-chunk + dedup check)'
-    traffic, traffic_src = pmc_traffic(args, n, size)
     result = None
     if rank == 0:
+        from replicat_amd.chunker import build_id
+        bid = build_id()
+        traffic, traffic_src = pmc_traffic(args.config, n, size, bid) if args.key == 'ff' \
+            else (None, 'seeded key: no PMC summary')
+        roof = roofline(bytes_per_step, bytes_needed(max_len, lens, last), tile_ms / calls,
+                        edge_ms / calls, chain_ms / calls, traffic, traffic_src, bid)
         cpu = None
-        if args.cpu_streams and world == 1 and args.key == 'ff' and args.config == '2':
-            cpu, cpu_ends = cpu_baseline(min(args.cpu_streams, n), size, synth.DEFAULT_SEED,
-                                         args.cpu_procs)
+        if world == 1 and args.key == 'ff' and args.config == '2' and args.cpu_streams != 0:
+            procs, seen = cpu_share()
+            procs = args.cpu_procs or procs
+            sample = min(args.cpu_streams or n, n)
+            cpu, cpu_ends = cpu_baseline(sample, size, synth.DEFAULT_SEED, procs)
+            cpu['affinity_cores'] = seen
             if ends is not None:
-                same = all(np.array_equal(np.asarray(cpu_ends[i], np.uint64), ends[i])
-                           for i in cpu_ends)
-                cpu['matches_gpu'] = bool(same)
-        e2e = None
-        if args.e2e and long is None:  # host-resident streams: copies in, chunking, cut offsets out
-            m = min(n, 64)
-            hbufs = [synth.stream_bytes(size, synth.DEFAULT_SEED, i) for i in range(m)]
-            pinned = torch.empty(m * size, dtype=torch.uint8).pin_memory()
-            pv = pinned.numpy()
-            for i, b in enumerate(hbufs):
-                pv[i * size:(i + 1) * size] = b
-            pbufs = [pv[i * size:(i + 1) * size] for i in range(m)]
-            e2e = {}
-            for label, bufs in (('pageable', hbufs), ('pinned', pbufs)):
-                ch.chunk_host(bufs[:2])
-                t1 = time.perf_counter()
-                ch.chunk_host(bufs)
-                e2e[label] = round(m * size / (time.perf_counter() - t1) / GIB, 2)
-            e2e['streams'] = m
-        calib = None
-        if args.calibrate:
-            out = torch.zeros(4, dtype=torch.int32, device='cuda')
-            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            probe = sum(lens) // 16 * 16
-            for _ in range(2):
-                read_probe(base_ptr, probe, out.data_ptr(), hs)
-            ev0.record(stream)
-            for _ in range(5):
-                read_probe(base_ptr, probe, out.data_ptr(), hs)
-            ev1.record(stream)
-            torch.cuda.synchronize()
-            calib = round(5 * probe / (ev0.elapsed_time(ev1) * 1e-3) / 1e9, 1)
+                cpu['matches_gpu'] = bool(all(np.array_equal(np.asarray(cpu_ends[i], np.uint64),
+                                                             ends[i]) for i in cpu_ends))
+        elif harness is not None and args.cpu_streams != 0 and world == 1:
+            cpu, lengths = harness_cpu(harness, min_len, max_len)
+            if cpu is not None and ends is not None:
+                cpu['matches_gpu'] = bool(np.array_equal(np.cumsum(lengths).astype(np.uint64),
+                                                         ends[0]))
         result = {
             'metric': 'GiB/s chunked, device-resident streams',
             'value': round(value, 2),
@@ -484,28 +696,65 @@ def main():
             'scaling': 'weak',
             'vs_baseline': None,
             'dtype': 'u8',
-            'data': 'synthetic (splitmix64 counter streams generated in HBM)',
-            'config': {'workload': workload,
-                       'streams_per_gpu': n, 'stream_bytes': size, 'parallelism': f'streams/{world} ranks'},
-            'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
-                         'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4),
-                         'traffic': None if traffic is None else round(traffic),
-                         'traffic_source': traffic_src,
-                         'algorithmic_bytes': bytes_per_step, 'kernel': 'rc_tile_kernel',
-                         'kernel_ms': round(a_avg, 3), 'chain_kernel_ms': round(b_avg, 3)},
+            'data': 'synthetic (splitmix64 counter streams generated in HBM)' if harness is None
+                    else 'synthetic (Random(0): the reference harness stream, copied to HBM)',
+            'config': {'workload': describe(args, long, n, size, min_len, max_len, world, edit),
+                       'streams_per_gpu': n, 'stream_bytes': size,
+                       'parallelism': f'streams/{world} ranks' if long is None
+                       else f'one stream split over {world} ranks'},
+            'roofline': roof,
             'cpu_baseline': cpu,
             'parity_sha256': parity,
+            'parity_scope': scope,
         }
+        if harness is not None:
+            result['rate_GBps'] = round(bytes_per_step * args.steps / elapsed / 1e9, 3)
         if edit is not None and getattr(edit, 'result', None) is not None:
             result['dedup'] = edit.result
-        if calib is not None:
-            result['read_probe_gbs'] = calib
-        if e2e is not None:
-            result['e2e_host_gibs'] = e2e
+        if args.e2e and long is None and harness is None:
+            result['e2e_host_gibs'] = e2e_rates(ch, n, size)
+        if args.calibrate:
+            result['read_probe_gbs'] = be.read_probe_gbs(base_ptr, sum(lens))
         print(json.dumps(result), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    ranks.barrier()
+    ranks.close()
     return result
+
+
+def describe(args, long, n, size, min_len, max_len, world, edit):
+    if long is not None:
+        return ('config3ii: ONE stream of %d GiB (last piece = final 1 MiB) split over %d '
+                'rank(s), min %d, max %d, key %s' % (long.L >> 30, world, min_len, max_len,
+                                                     args.key))
+    if args.config == 'harness':
+        return ('harness: Repository._benchmark_chunker stream, 10 x 512,000,000 B Random(0) '
+                'as one stream of 10 pieces, min %d, max %d' % (min_len, max_len))
+    w = ('config%s: %d x %d MiB streams per GPU, min %d, max %d, key %s'
+         % (args.config, n, size >> 20, min_len, max_len, args.key))
+    if edit is not None:
+        w += ' (512 of the 1024 edited, re-chunk + dedup check)'
+    return w
+
+
+def e2e_rates(ch, n, size):
+    """Host-resident streams: pinned copies in, chunking, cut offsets out (rc_chunk_host)."""
+    import torch
+    from replicat_amd import synth
+    m = min(n, 64)
+    hbufs = [synth.stream_bytes(size, synth.DEFAULT_SEED, i) for i in range(m)]
+    pinned = torch.empty(m * size, dtype=torch.uint8).pin_memory()
+    pv = pinned.numpy()
+    for i, b in enumerate(hbufs):
+        pv[i * size:(i + 1) * size] = b
+    pbufs = [pv[i * size:(i + 1) * size] for i in range(m)]
+    out = {}
+    for label, bufs in (('pageable', hbufs), ('pinned', pbufs)):
+        ch.chunk_host(bufs[:2])
+        t1 = time.perf_counter()
+        ch.chunk_host(bufs)
+        out[label] = round(m * size / (time.perf_counter() - t1) / GIB, 2)
+    out['streams'] = m
+    return out
 
 
 if __name__ == '__main__':

@@ -47,8 +47,12 @@ extern "C" {
 
 typedef struct rc_chunker rc_chunker;
 
-/* Library / ABI version, e.g. 100 = 0.1.0. */
+/* Library / ABI version, e.g. 200 = 0.2.0. */
 int rc_version(void);
+
+/* Build id: a hash over the library's sources and compile flags, set by replicat_amd/build.py
+ * ("unknown" for a build outside it).  Profiles record it so stale counters are refused. */
+const char *rc_build_id(void);
 
 /* Message of this thread's last error ("" if none). */
 const char *rc_last_error(void);
@@ -97,16 +101,25 @@ int rc_chunk_host(rc_chunker *ch, uint64_t n, const uint8_t *const *streams,
                   uint64_t *cuts, int64_t *counts);
 
 /* Kernel timing, for bench.py's roofline: while enabled, every rc_chunk_device call records
- * HIP events around its tile kernel (phase A) and its chain kernel (phase B) on the launch
- * stream.  rc_timing_read waits for the recorded events, returns the summed milliseconds and
- * the number of calls, and clears the record. */
+ * HIP events on the launch stream before the tile kernel, between it and the edge kernel, and
+ * around the chain kernels.  rc_timing_read_kernels waits for the recorded events, returns the
+ * summed milliseconds of each phase and the number of calls, and clears the record;
+ * rc_timing_read returns phase A = tile + edge and phase B = chain the same way. */
 int rc_timing_enable(rc_chunker *ch, int enable);
+int rc_timing_read_kernels(rc_chunker *ch, double *tile_ms, double *edge_ms, double *chain_ms,
+                           uint64_t *calls);
 int rc_timing_read(rc_chunker *ch, double *phase_a_ms, double *phase_b_ms, uint64_t *calls);
 
 /* Synthetic stream bytes on the device (replicat_amd/synth.py): word i of stream `stream`
  * is splitmix64((seed * 0x9E3779B97F4A7C15) ^ (stream << 34) ^ i), little-endian. */
 int rc_fill_splitmix(uint8_t *d_dst, uint64_t nbytes, uint64_t seed, uint64_t stream,
                      void *hip_stream);
+/* n streams at once, stream k (id first_stream + k * stream_step) at d_dst + k * slot; slot
+ * is a multiple of 8 of at least nbytes rounded up to 8 (a stream's last word is written whole,
+ * into the slot's slack).  One launch for a whole arena of synthetic streams. */
+int rc_fill_splitmix_streams(uint8_t *d_dst, uint64_t n, uint64_t nbytes, uint64_t slot,
+                             uint64_t seed, uint64_t first_stream, uint64_t stream_step,
+                             void *hip_stream);
 /* The same bytes from word `word0` of the stream on (byte offset 8 * word0): one segment of a
  * long stream (the multi-device split of a single stream, replicat_amd/split.py). */
 int rc_fill_splitmix_at(uint8_t *d_dst, uint64_t nbytes, uint64_t seed, uint64_t stream,
@@ -127,13 +140,16 @@ uint64_t rc_host_key(const rc_chunker *ch, uint64_t d);
 
 /* Inspection (tests): run only the per-tile phase (tile + edge kernels) over device streams and
  * copy the tile records to host arrays: for tile t of the concatenated tile list (stream i's
- * tiles start at the exclusive prefix sum of ceil((jneed_i + 1) / rc_tile_keys())), keys[t] =
- * the first maximal 64-bit key among the tile's needed keys (0 if none is positive) and
- * js[t] = its key index in the stream.  *n_tiles receives the tile count; at most cap are
- * copied.  Blocking. */
+ * tiles start at the exclusive prefix sum of jneed_i / rc_tile_keys() + 1), keys[t] = the first
+ * maximal 64-bit key among the tile's keys (0 if none is positive) and js[t] = its key index in
+ * the stream.  A tile's keys are all of j0 .. j0 + rc_tile_keys() - 1 when their bytes lie in
+ * the stream, else those up to jneed; key 0 never counts.  gmax (may be NULL): for chunkers
+ * with small windows (max_length below ~1 MB) the top-16 maximum of each quarter of the tile
+ * (u16 q at bits 16q), ~0 for a tile computed exactly or a chunker without them.  *n_tiles
+ * receives the tile count; at most cap are copied.  Blocking. */
 int rc_tile_records(rc_chunker *ch, uint64_t n, const uint8_t *const *d_streams,
                     const uint64_t *lens, const uint64_t *last_piece, uint64_t *keys,
-                    uint64_t *js, uint64_t cap, uint64_t *n_tiles);
+                    uint64_t *js, uint64_t *gmax, uint64_t cap, uint64_t *n_tiles);
 uint64_t rc_tile_keys(void);
 
 /* Host-only check of the table construction (no device needed): out[i] = key of data word

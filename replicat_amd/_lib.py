@@ -34,6 +34,7 @@ RC_DIGEST_SLOT = 64
 _u64, _i64, _u32, _int, _p = ctypes.c_uint64, ctypes.c_int64, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p
 SIGNATURES = {
     'rc_version': (_int, []),
+    'rc_build_id': (ctypes.c_char_p, []),
     'rc_last_error': (ctypes.c_char_p, []),
     'rc_chunker_create': (_int, [_u64, _u64, _p, _u64, _int, ctypes.POINTER(_p)]),
     'rc_chunker_destroy': (None, [_p]),
@@ -46,13 +47,17 @@ SIGNATURES = {
     'rc_timing_enable': (_int, [_p, _int]),
     'rc_timing_read': (_int, [_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                               ctypes.POINTER(_u64)]),
+    'rc_timing_read_kernels': (_int, [_p, ctypes.POINTER(ctypes.c_double),
+                                      ctypes.POINTER(ctypes.c_double),
+                                      ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_u64)]),
     'rc_fill_splitmix': (_int, [_p, _u64, _u64, _u64, _p]),
     'rc_fill_splitmix_at': (_int, [_p, _u64, _u64, _u64, _u64, _p]),
+    'rc_fill_splitmix_streams': (_int, [_p, _u64, _u64, _u64, _u64, _u64, _u64, _p]),
     'rc_read_probe': (_int, [_p, _u64, _p, _p]),
     'rc_keys_needed': (_u64, [_u64, _u64, _u64]),
     'rc_host_key': (_u64, [_p, _u64]),
     'rc_tables_key': (_int, [_p, _u64, _p, _p, _p]),
-    'rc_tile_records': (_int, [_p, _u64, _p, _p, _p, _p, _p, _u64, ctypes.POINTER(_u64)]),
+    'rc_tile_records': (_int, [_p, _u64, _p, _p, _p, _p, _p, _p, _u64, ctypes.POINTER(_u64)]),
     'rc_tile_keys': (_u64, []),
     # replicat_digest.h
     'rc_blake2b_create': (_int, [_u32, _int, ctypes.POINTER(_p)]),

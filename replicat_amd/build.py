@@ -1,9 +1,17 @@
 """Build libreplicat_chunker.so in-tree: hipcc, gfx950 only, no torch extension machinery.
 
-    python -m replicat_amd.build        (also run by __graft_entry__.build())
-    python -m replicat_amd.build --diag (+ the GCM watchdog harness under diag/)
+    python -m replicat_amd.build            (also run by __graft_entry__.build() and setup.py)
+    python -m replicat_amd.build --force
+    python -m replicat_amd.build --variant STAMPS -DRC_DIAG_STAMPS   (diag/lib_STAMPS.so)
+    python -m replicat_amd.build --diag     (+ the GCM watchdog harness under diag/)
+
+Staleness is decided by content, not mtime: the library embeds a build id -- a hash over every
+source and header and the compile command -- and a library whose id differs from the tree's is
+rebuilt (``rc_build_id()`` returns it at run time; profiles record it).
 """
+import hashlib
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -17,6 +25,8 @@ SOURCES = [os.path.join(CSRC, n) for n in ('kernels.hip', 'capi.cpp', 'blake2b.h
 HEADERS = [os.path.join(CSRC, n) for n in ('gclmul.h', 'digest_kernels.h', 'capi_internal.h', 'cipher_kernels.h')] + [
     os.path.join(ROOT, 'include', n) for n in ('replicat_chunker.h', 'replicat_digest.h', 'replicat_cipher.h')]
 ARCH = 'gfx950'
+FLAGS = [f'--offload-arch={ARCH}', '-O3', '-std=c++17', '-fPIC', '-shared', '-Wall']
+_ID_RE = re.compile(rb'RC_BUILD_ID:([0-9a-f]{16})')
 
 
 def hipcc():
@@ -26,23 +36,57 @@ def hipcc():
     raise RuntimeError('hipcc not found (ROCm 7.x required)')
 
 
-def stale():
-    if not os.path.exists(LIB):
-        return True
-    t = os.path.getmtime(LIB)
-    return any(os.path.getmtime(p) > t for p in SOURCES + HEADERS)
+def source_id(extra=()):
+    """Hash of every source/header (path relative to the package) and the compile flags."""
+    h = hashlib.sha256()
+    for p in SOURCES + HEADERS:
+        h.update(os.path.relpath(p, ROOT).encode() + b'\0')
+        with open(p, 'rb') as f:
+            h.update(f.read())
+    h.update(' '.join(FLAGS + list(extra)).encode())
+    return h.hexdigest()[:16]
+
+
+def embedded_id(path=LIB):
+    """The build id compiled into a library file, or None."""
+    try:
+        with open(path, 'rb') as f:
+            m = _ID_RE.search(f.read())
+    except OSError:
+        return None
+    return m.group(1).decode() if m else None
+
+
+def stale(path=LIB, extra=()):
+    return embedded_id(path) != source_id(extra)
+
+
+def _compile(out, extra=(), verbose=False):
+    bid = source_id(extra)
+    cmd = [hipcc(), *FLAGS, *extra, f'-DRC_BUILD_ID="{bid}"', '-I', os.path.join(ROOT, 'include'),
+           *SOURCES, '-o', out + '.tmp']
+    if verbose:
+        print(' '.join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(out + '.tmp', out)
+    return out
 
 
 def build(force=False, verbose=False):
     if not force and not stale():
         return LIB
-    cmd = [hipcc(), f'--offload-arch={ARCH}', '-O3', '-std=c++17', '-fPIC', '-shared', '-Wall',
-           '-I', os.path.join(ROOT, 'include'), *SOURCES, '-o', LIB + '.tmp']
-    if verbose:
-        print(' '.join(cmd), flush=True)
-    subprocess.run(cmd, check=True)
-    os.replace(LIB + '.tmp', LIB)
-    return LIB
+    return _compile(LIB, verbose=verbose)
+
+
+def build_variant(name, defines, verbose=False):
+    """A diagnostic build (e.g. -DRC_DIAG_STAMPS) as diag/lib_<name>.so, loaded through
+    RC_LIB_PATH by the diagnostics scripts only."""
+    out_dir = os.path.join(ROOT, 'diag')
+    os.makedirs(out_dir, exist_ok=True)
+    out = os.path.join(out_dir, f'lib_{name}.so')
+    if stale(out, defines):
+        _compile(out, defines, verbose)
+    return out
 
 
 def build_diag(verbose=False):
@@ -61,6 +105,10 @@ def build_diag(verbose=False):
 
 
 if __name__ == '__main__':
-    build(force='--force' in sys.argv, verbose=True)
+    if '--variant' in sys.argv:
+        i = sys.argv.index('--variant')
+        build_variant(sys.argv[i + 1], [a for a in sys.argv[i + 2:] if a.startswith('-D')], True)
+    else:
+        build(force='--force' in sys.argv, verbose=True)
     if '--diag' in sys.argv:
         build_diag(verbose=True)

@@ -107,18 +107,22 @@ class GpuChunker:
         base = np.concatenate([[0], np.cumsum(caps)[:-1]]).astype(np.int64)
         return [cuts[b:b + c] for b, c in zip(base, counts)]
 
-    def tile_records(self, ptrs, lens, last_piece=None):
-        """(keys, js) of the per-tile phase over device streams (inspection / tests)."""
+    def tile_records(self, ptrs, lens, last_piece=None, groups=False):
+        """(keys, js) of the per-tile phase over device streams (inspection / tests); with
+        groups=True also the per-quarter top-16 maxima (keys, js, gmax)."""
         ptrs, lens = _ptr_array(ptrs), _ptr_array(lens)
         last = _ptr_array(last_piece if last_piece is not None else np.zeros(len(lens)))
         nt = ctypes.c_uint64()
         check(lib().rc_tile_records(self._h, len(lens), ptrs.ctypes.data, lens.ctypes.data,
-                                    last.ctypes.data, None, None, 0, ctypes.byref(nt)))
+                                    last.ctypes.data, None, None, None, 0, ctypes.byref(nt)))
         keys = np.zeros(max(nt.value, 1), dtype=np.uint64)
         js = np.zeros(max(nt.value, 1), dtype=np.uint64)
+        gm = np.zeros(max(nt.value, 1), dtype=np.uint64)
         check(lib().rc_tile_records(self._h, len(lens), ptrs.ctypes.data, lens.ctypes.data,
                                     last.ctypes.data, keys.ctypes.data, js.ctypes.data,
-                                    nt.value, ctypes.byref(nt)))
+                                    gm.ctypes.data, nt.value, ctypes.byref(nt)))
+        if groups:
+            return keys[:nt.value], js[:nt.value], gm[:nt.value]
         return keys[:nt.value], js[:nt.value]
 
     # ---------------------------------------------------------------------- profiling
@@ -127,13 +131,28 @@ class GpuChunker:
         check(lib().rc_timing_enable(self._h, 1 if enable else 0))
 
     def read_timing(self):
+        """(tile + edge ms, chain ms, calls) summed since the last read."""
         a, b, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_uint64()
         check(lib().rc_timing_read(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(n)))
         return a.value, b.value, n.value
 
+    def read_kernel_timing(self):
+        """(tile ms, edge ms, chain ms, calls) summed since the last read (HIP events on the
+        launch stream)."""
+        t, e, c = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        n = ctypes.c_uint64()
+        check(lib().rc_timing_read_kernels(self._h, ctypes.byref(t), ctypes.byref(e),
+                                           ctypes.byref(c), ctypes.byref(n)))
+        return t.value, e.value, c.value, n.value
+
 
 def tile_keys():
     return lib().rc_tile_keys()
+
+
+def build_id():
+    """The loaded library's build id (replicat_amd/build.py: hash of sources and flags)."""
+    return lib().rc_build_id().decode()
 
 
 def keys_needed(max_length, L, P):
@@ -142,6 +161,12 @@ def keys_needed(max_length, L, P):
 
 def fill_splitmix(ptr, nbytes, seed, stream_id, hip_stream=0):
     check(lib().rc_fill_splitmix(ptr, nbytes, seed, stream_id, hip_stream or None))
+
+
+def fill_splitmix_streams(ptr, n, nbytes, slot, seed, first_id, id_step=1, hip_stream=0):
+    """n synthetic streams of nbytes at ptr + k * slot (ids first_id + k * id_step), one launch."""
+    check(lib().rc_fill_splitmix_streams(ptr, n, nbytes, slot, seed, first_id, id_step,
+                                         hip_stream or None))
 
 
 def fill_splitmix_at(ptr, nbytes, seed, stream_id, word0, hip_stream=0):

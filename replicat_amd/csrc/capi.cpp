@@ -159,6 +159,7 @@ int rc_fail(int code, const char *fmt, ...) {
 
 struct rc_chunker {
     uint64_t min_length = 0, max_length = 0, window = 0;
+    bool groups = false;  // small windows: the tile kernel also writes per-group maxima
     uint64_t seg_force = 0, ext_steps = 2;  // segment-parallel chains (see stage_descriptors)
     uint64_t k0 = 0, k1 = 0;
     int device = 0;
@@ -186,10 +187,15 @@ struct rc_chunker {
     DevBuf d_stage[2], d_hcuts[2], d_hcounts[2], d_hdig[2];
     hipStream_t hstream[2] = {nullptr, nullptr};
 
-    // timing
+    // descriptor uploads run on their own stream, so that a call's upload overlaps the
+    // previous call's kernels (the workspace alternation keeps the two apart)
+    hipStream_t cstream = nullptr;
+    hipEvent_t uploaded[2] = {nullptr, nullptr};
+
+    // timing: events before the tile kernel, after it, after the edge kernel, after the chain
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;
-    std::vector<std::array<hipEvent_t, 3>> ev_rec;
+    std::vector<std::array<hipEvent_t, 4>> ev_rec;
 };
 
 namespace {
@@ -333,16 +339,30 @@ int stage_descriptors(rc_chunker *ch, Workspace &ws, uint64_t n, const uint8_t *
     return 0;
 }
 
+uint64_t *group_maxima(Workspace &ws, const Plan &plan) {
+    return reinterpret_cast<uint64_t *>(static_cast<char *>(ws.d_records.p) +
+                                        (plan.n_tiles + 1) * sizeof(TileRecord));
+}
+
 int upload_and_launch(rc_chunker *ch, Workspace &ws, const Plan &plan, ChainParams prm,
                       uint64_t *d_cuts, int64_t *d_counts, hipStream_t stream) {
     if (int rc = ws.d_desc.ensure(plan.bytes)) return rc;
-    if (int rc = ws.d_records.ensure((plan.n_tiles + 1) * sizeof(TileRecord))) return rc;
+    // records, then (small windows) the group maxima of every tile
+    if (int rc = ws.d_records.ensure((plan.n_tiles + 1) * (sizeof(TileRecord) + 8))) return rc;
     if (int rc = ws.d_scratch.ensure(std::max<uint64_t>(plan.scratch_entries, 1) * 8)) return rc;
     // counts, merge points, slice offsets and slices of the parallel join (kernels.hip)
     if (int rc = ws.d_seg_counts.ensure(std::max<uint64_t>(plan.n_segs, 1) * 32)) return rc;
-    HIP_TRY(hipMemcpyAsync(ws.d_desc.p, ws.h_desc.p, plan.bytes, hipMemcpyHostToDevice, stream));
+    // The upload goes on the copy stream: stage_descriptors already waited for the call that
+    // last used this workspace, so its device buffer is free now, while the previous call's
+    // kernels may still be running on `stream`.  `stream` waits for the upload only.
+    const int wi = &ws == &ch->ws[0] ? 0 : 1;
+    if (!ch->cstream) HIP_TRY(hipStreamCreateWithFlags(&ch->cstream, hipStreamNonBlocking));
+    if (!ch->uploaded[wi]) HIP_TRY(hipEventCreateWithFlags(&ch->uploaded[wi], hipEventDisableTiming));
+    HIP_TRY(hipMemcpyAsync(ws.d_desc.p, ws.h_desc.p, plan.bytes, hipMemcpyHostToDevice, ch->cstream));
+    HIP_TRY(hipEventRecord(ch->uploaded[wi], ch->cstream));
+    HIP_TRY(hipStreamWaitEvent(stream, ch->uploaded[wi], 0));
     const StreamDesc d = desc_view(ws.d_desc.p, plan.n);
-    std::array<hipEvent_t, 3> ev{};
+    std::array<hipEvent_t, 4> ev{};
     if (ch->timing) {
         for (auto &e : ev) {
             if (ch->ev_pool.empty()) {
@@ -354,10 +374,13 @@ int upload_and_launch(rc_chunker *ch, Workspace &ws, const Plan &plan, ChainPara
         }
         HIP_TRY(hipEventRecord(ev[0], stream));
     }
+    uint64_t *gmax = ch->groups ? group_maxima(ws, plan) : nullptr;
+    prm.gmax = gmax;
     if (rc_launch_tiles(ch->d_tables, d, plan.n, plan.n_tiles,
-                        static_cast<TileRecord *>(ws.d_records.p), stream))
+                        static_cast<TileRecord *>(ws.d_records.p), gmax, stream,
+                        ch->timing ? ev[1] : nullptr))
         return fail(RC_ERR_HIP, "%s", rc_launch_error());
-    if (ch->timing) HIP_TRY(hipEventRecord(ev[1], stream));
+    if (ch->timing) HIP_TRY(hipEventRecord(ev[2], stream));
     if (rc_launch_chain(ch->d_tables, d, plan.n, prm, plan.n_segs,
                         static_cast<const TileRecord *>(ws.d_records.p), d_cuts, d_counts,
                         static_cast<uint64_t *>(ws.d_scratch.p),
@@ -366,7 +389,7 @@ int upload_and_launch(rc_chunker *ch, Workspace &ws, const Plan &plan, ChainPara
     HIP_TRY(hipEventRecord(ws.done, stream));
     ws.pending = true;
     if (ch->timing) {
-        HIP_TRY(hipEventRecord(ev[2], stream));
+        HIP_TRY(hipEventRecord(ev[3], stream));
         ch->ev_rec.push_back(ev);
     }
     return 0;
@@ -383,6 +406,7 @@ ChainParams chain_params(const rc_chunker *ch, const Plan &plan, uint64_t max_st
     p.seg_bytes = plan.seg_bytes;
     p.seg_cap = plan.seg_cap;
     p.ext_steps = ch->ext_steps;
+    p.gmax = nullptr;  // set per launch (upload_and_launch)
     return p;
 }
 
@@ -390,7 +414,15 @@ ChainParams chain_params(const rc_chunker *ch, const Plan &plan, uint64_t max_st
 
 extern "C" {
 
-int rc_version(void) { return 100; }
+int rc_version(void) { return 200; }
+
+#ifndef RC_BUILD_ID
+#define RC_BUILD_ID "unknown"
+#endif
+// "RC_BUILD_ID:" + the hash replicat_amd/build.py computes over the sources and flags; the
+// marker lets build.py read it from the .so file without loading it
+static const char kBuildId[] = "RC_BUILD_ID:" RC_BUILD_ID;
+const char *rc_build_id(void) { return kBuildId + 12; }
 
 const char *rc_last_error(void) { return g_err; }
 
@@ -439,6 +471,10 @@ int rc_chunker_create(uint64_t min_length, uint64_t max_length, const uint8_t *k
     ch->min_length = min_length;
     ch->max_length = max_length;
     ch->window = window_keys(max_length);
+    // a window (plus its two edge tiles) within one 64-tile row of the chain's record cache:
+    // the chain's edge ranges are then a large part of its work, and group maxima trim them
+    ch->groups = ch->window / kTileKeys + 3 <= 64;
+    if (const char *e = getenv("RC_TILE_GROUPS_OFF")) ch->groups = ch->groups && e[0] != '1';
     ch->k0 = k0;
     ch->k1 = k1;
     ch->device = device;
@@ -490,6 +526,9 @@ void rc_chunker_destroy(rc_chunker *ch) {
             if (ch->hstream[i]) (void)hipStreamDestroy(ch->hstream[i]);
         }
         ch->h_out.release();
+        if (ch->cstream) (void)hipStreamDestroy(ch->cstream);
+        for (auto e : ch->uploaded)
+            if (e) (void)hipEventDestroy(e);
         for (auto &r : ch->ev_rec)
             for (auto e : r) (void)hipEventDestroy(e);
         for (auto e : ch->ev_pool) (void)hipEventDestroy(e);
@@ -721,7 +760,7 @@ uint64_t rc_tile_keys(void) { return kTileKeys; }
 
 int rc_tile_records(rc_chunker *ch, uint64_t n, const uint8_t *const *d_streams,
                     const uint64_t *lens, const uint64_t *last_piece, uint64_t *keys,
-                    uint64_t *js, uint64_t cap, uint64_t *n_tiles) {
+                    uint64_t *js, uint64_t *gmax, uint64_t cap, uint64_t *n_tiles) {
     if (!ch || !n_tiles) return fail(RC_ERR_ARGUMENT, "null argument");
     if (int rc = validate_streams(n, d_streams, lens, last_piece, true)) return rc;
     std::lock_guard<std::mutex> lock(ch->mu);
@@ -730,20 +769,25 @@ int rc_tile_records(rc_chunker *ch, uint64_t n, const uint8_t *const *d_streams,
     Workspace &ws = acquire_ws(ch);
     if (int rc = stage_descriptors(ch, ws, n, d_streams, lens, last_piece, plan)) return rc;
     if (int rc = ws.d_desc.ensure(plan.bytes)) return rc;
-    if (int rc = ws.d_records.ensure((plan.n_tiles + 1) * sizeof(TileRecord))) return rc;
+    if (int rc = ws.d_records.ensure((plan.n_tiles + 1) * (sizeof(TileRecord) + 8))) return rc;
     HIP_TRY(hipMemcpy(ws.d_desc.p, ws.h_desc.p, plan.bytes, hipMemcpyHostToDevice));
+    uint64_t *d_gmax = ch->groups ? group_maxima(ws, plan) : nullptr;
     if (rc_launch_tiles(ch->d_tables, desc_view(ws.d_desc.p, n), n, plan.n_tiles,
-                        static_cast<TileRecord *>(ws.d_records.p), nullptr))
+                        static_cast<TileRecord *>(ws.d_records.p), d_gmax, nullptr, nullptr))
         return fail(RC_ERR_HIP, "%s", rc_launch_error());
     HIP_TRY(hipDeviceSynchronize());
     std::vector<TileRecord> h(plan.n_tiles);
-    if (plan.n_tiles)
+    std::vector<uint64_t> hg(plan.n_tiles, ~0ull);
+    if (plan.n_tiles) {
         HIP_TRY(hipMemcpy(h.data(), ws.d_records.p, plan.n_tiles * sizeof(TileRecord),
                           hipMemcpyDeviceToHost));
+        if (d_gmax) HIP_TRY(hipMemcpy(hg.data(), d_gmax, plan.n_tiles * 8, hipMemcpyDeviceToHost));
+    }
     *n_tiles = plan.n_tiles;
     for (uint64_t t = 0; t < plan.n_tiles && t < cap; ++t) {
         keys[t] = h[t].key;
         js[t] = h[t].j;
+        if (gmax) gmax[t] = hg[t];
     }
     return RC_OK;
 }
@@ -754,24 +798,34 @@ int rc_timing_enable(rc_chunker *ch, int enable) {
     return RC_OK;
 }
 
-int rc_timing_read(rc_chunker *ch, double *phase_a_ms, double *phase_b_ms, uint64_t *calls) {
+int rc_timing_read_kernels(rc_chunker *ch, double *tile_ms, double *edge_ms, double *chain_ms,
+                           uint64_t *calls) {
     if (!ch) return fail(RC_ERR_ARGUMENT, "null chunker");
     std::lock_guard<std::mutex> lock(ch->mu);
     DeviceGuard g(ch->device);
-    double a = 0, b = 0;
+    double t[3] = {0, 0, 0};
     for (auto &r : ch->ev_rec) {
-        HIP_TRY(hipEventSynchronize(r[2]));
-        float x = 0, y = 0;
-        HIP_TRY(hipEventElapsedTime(&x, r[0], r[1]));
-        HIP_TRY(hipEventElapsedTime(&y, r[1], r[2]));
-        a += x;
-        b += y;
+        HIP_TRY(hipEventSynchronize(r[3]));
+        for (int k = 0; k < 3; ++k) {
+            float x = 0;
+            HIP_TRY(hipEventElapsedTime(&x, r[k], r[k + 1]));
+            t[k] += x;
+        }
         for (auto e : r) ch->ev_pool.push_back(e);
     }
-    if (phase_a_ms) *phase_a_ms = a;
-    if (phase_b_ms) *phase_b_ms = b;
+    if (tile_ms) *tile_ms = t[0];
+    if (edge_ms) *edge_ms = t[1];
+    if (chain_ms) *chain_ms = t[2];
     if (calls) *calls = ch->ev_rec.size();
     ch->ev_rec.clear();
+    return RC_OK;
+}
+
+int rc_timing_read(rc_chunker *ch, double *phase_a_ms, double *phase_b_ms, uint64_t *calls) {
+    double tile = 0, edge = 0, chain = 0;
+    if (int rc = rc_timing_read_kernels(ch, &tile, &edge, &chain, calls)) return rc;
+    if (phase_a_ms) *phase_a_ms = tile + edge;
+    if (phase_b_ms) *phase_b_ms = chain;
     return RC_OK;
 }
 
@@ -785,6 +839,19 @@ int rc_read_probe(const uint8_t *d_src, uint64_t nbytes, uint32_t *d_out, void *
 int rc_fill_splitmix(uint8_t *d_dst, uint64_t nbytes, uint64_t seed, uint64_t stream, void *hip_stream) {
     if (nbytes && !d_dst) return fail(RC_ERR_ARGUMENT, "null destination");
     if (rc_launch_fill(d_dst, nbytes, seed, stream, 0, hip_stream)) return fail(RC_ERR_HIP, "%s", rc_launch_error());
+    return RC_OK;
+}
+
+int rc_fill_splitmix_streams(uint8_t *d_dst, uint64_t n, uint64_t nbytes, uint64_t slot,
+                             uint64_t seed, uint64_t first_stream, uint64_t stream_step,
+                             void *hip_stream) {
+    if (n && nbytes && !d_dst) return fail(RC_ERR_ARGUMENT, "null destination");
+    if (slot % 8 || slot < ((nbytes + 7) & ~7ull))
+        return fail(RC_ERR_ARGUMENT, "slot %llu must be a multiple of 8 holding %llu bytes",
+                    (unsigned long long)slot, (unsigned long long)nbytes);
+    if (reinterpret_cast<uintptr_t>(d_dst) & 7) return fail(RC_ERR_ALIGN, "destination not 8-byte aligned");
+    if (rc_launch_fill_streams(d_dst, n, nbytes, slot, seed, first_stream, stream_step, hip_stream))
+        return fail(RC_ERR_HIP, "%s", rc_launch_error());
     return RC_OK;
 }
 

@@ -23,6 +23,11 @@ constexpr int kTileKeys = 64 * 4 * kTileIters;  // keys per tile = one wave: 64 
 constexpr int kWaveSize = 64;
 constexpr int kTileWaves = 16;       // waves per workgroup of the tile kernel (1024 threads)
 constexpr int kChainWaves = 4;       // waves (= streams) per workgroup of the chain kernel
+#ifndef RC_TILE_GROUPS
+#define RC_TILE_GROUPS 4
+#endif
+constexpr int kTileGroups = RC_TILE_GROUPS;  // key groups per tile with group maxima (<= 4: one u64)
+constexpr int kGroupKeys = kTileKeys / kTileGroups;
 
 // ---- LDS image of the tile kernel -------------------------------------------------------
 // Prefilter tables replicated 32x so that the 32 lanes of each ds_read_b32 lane group each own
@@ -68,6 +73,7 @@ struct ChainParams {
     uint64_t seg_bytes;   // chain segment length (multiple of 4)
     uint64_t seg_cap;     // entries per speculative list
     uint64_t ext_steps;   // steps a speculative chain runs past its segment end
+    const uint64_t *gmax; // per-tile group maxima (rc_launch_tiles), or NULL
     uint32_t open;        // RC_OPEN: non-final prefix, no tail rule
 };
 
@@ -84,14 +90,20 @@ __host__ __device__ inline uint64_t splitmix64(uint64_t x) {
 // Launchers implemented in kernels.hip (host-callable, enqueue only).
 extern "C" {
 // d_records: n_tiles + 1 entries (the last is scratch for the tile kernel's pipeline)
+// d_gmax (may be NULL): n_tiles + 1 words of per-group top-16 maxima (kTileGroups x u16 per
+// tile) -- the chain's bounds for small windows.  mid_event (a hipEvent_t, may be NULL):
+// recorded between the tile and the edge kernel.
 int rc_launch_tiles(const rc::KeyTables *d_tables, rc::StreamDesc desc, uint64_t n_streams,
-                    uint64_t n_tiles, rc::TileRecord *d_records, void *stream);
+                    uint64_t n_tiles, rc::TileRecord *d_records, uint64_t *d_gmax, void *stream,
+                    void *mid_event);
 int rc_launch_chain(const rc::KeyTables *d_tables, rc::StreamDesc desc, uint64_t n_streams,
                     rc::ChainParams prm, uint64_t n_segs, const rc::TileRecord *d_records,
                     uint64_t *d_cuts, int64_t *d_counts, uint64_t *d_scratch,
                     uint64_t *d_seg_counts, bool any_multi, void *stream);
 int rc_launch_fill(uint8_t *d_dst, uint64_t nbytes, uint64_t seed, uint64_t stream_id,
                    uint64_t word0, void *stream);
+int rc_launch_fill_streams(uint8_t *d_dst, uint64_t n, uint64_t nbytes, uint64_t slot,
+                           uint64_t seed, uint64_t id0, uint64_t id_step, void *stream);
 int rc_launch_read_probe(const uint8_t *d_src, uint64_t nbytes, uint32_t *d_out, void *stream);
 const char *rc_launch_error(void);
 }

@@ -253,13 +253,30 @@ __device__ __forceinline__ void scan_records(const TileRecord *rec, uint64_t t_l
     }
 }
 
-// Where a wave's tile lives.  `fast` = a full interior tile (keys j0 .. j0+4095 all needed,
-// j0 >= kTileKeys); tile 0 and a partial last tile of every stream go to the edge kernel.
+// Where a wave's tile lives.  `fast` = every key j0 .. j0+4095 has its 8 bytes inside the
+// stream (tile_fast below): the tile kernel's register ring reads exactly those 16 KiB.
+// Tile 0 is fast too (its key 0, which would need the word before the stream, is masked out of
+// the scan), and so is a stream's last tile when it ends inside the data: its keys past `jneed`
+// are real keys no argmax window reaches, so its record is the first maximum over a superset of
+// the keys the chain asks about -- which the chain only ever uses as that tile's exact answer
+// when the record's index lies inside the asked range, and otherwise as an upper bound (see
+// chain_step), both of which hold for a superset.  Only a last tile that runs past the stream's
+// final word goes to the edge kernel (it happens when jneed is within 4096 keys of the end).
 struct TileRef {
     const uint8_t *base;
     uint64_t j0;
     bool fast;
 };
+
+// j0 + 4095 <= jmax, with jmax = (L - 4) / 4 the last key whose 8 bytes exist (adapters.cpp:73)
+__device__ __forceinline__ bool tile_fast(uint64_t j0, uint64_t L) {
+    return L >= 8 && j0 + kTileKeys - 1 <= (L - 4) / 4;
+}
+
+// Last key index of a tile's record: the whole tile on the fast path, else clipped to jneed.
+__device__ __forceinline__ uint64_t tile_key_end(uint64_t j0, uint64_t L, uint64_t jneed) {
+    return tile_fast(j0, L) ? j0 + kTileKeys - 1 : min(j0 + kTileKeys - 1, jneed);
+}
 
 constexpr uint32_t kLastLocal = 4 * kTileIters - 1;
 constexpr uint64_t kTieMark = ~0ull;  // TileRecord.j of a tile left to the exact path  // a lane's keys in a tile: 0 .. kLastLocal
@@ -272,18 +289,34 @@ constexpr uint64_t kTieMark = ~0ull;  // TileRecord.j of a tile left to the exac
 // Returns the lane's largest top-16 value and the first and last local index where it occurs.
 // `prev_word` holds the word before the tile (key j0's low half) and is refilled with the next
 // tile's, issued with the ring.
+//
+// G > 1 (chunkers with small windows, see rc_launch_tiles): the tile's keys also fall into G
+// groups of kTileKeys / G consecutive keys (iterations it * G / kTileIters), and the lane's
+// largest top-16 value per group comes back packed two per word in gpk (group g in half g & 1
+// of gpk[g / 2]).  The per-lane maximum then accumulates per group and folds into acc_first at
+// each group's end: one extra v_max per group, not per key.
+template <int G>
 __device__ __forceinline__ void tile_scan(const TileRef &tr, const TileRef &nx,
                                           u32x4 (&x)[kTileIters], uint32_t &prev_word,
                                           uint32_t lb_a, uint32_t lb_b, uint32_t &top,
-                                          uint32_t &first, uint32_t &last) {
+                                          uint32_t &first, uint32_t &last,
+                                          uint32_t (&gpk)[(G + 1) / 2]) {
+    static_assert(G == 1 || (G % 2 == 0 && kTileIters % G == 0), "groups: 1 or an even divisor");
+    constexpr int kPer = kTileIters / G;  // iterations per group
     const uint32_t lane = lane_id();
     // no next fast tile (end of the wave's range): harmlessly re-read this tile instead, so
     // the ring loads stay unconditional
     const uint8_t *nbase = nx.fast ? nx.base + 4 * nx.j0 : tr.base + 4 * tr.j0;
     const __amdgpu_buffer_rsrc_t nsrc = tile_rsrc(nbase);
     uint32_t carry = pf_entry(prev_word, lb_a, lb_b);
-    prev_word = ld_u32(nbase - 4);
-    uint32_t acc_first = 0, acc_last = 0;
+    // the word before the next tile; a stream's tile 0 has none (its key 0 is masked below),
+    // so it re-reads its own first word rather than the 4 bytes before the stream
+    const uint64_t nj0 = nx.fast ? nx.j0 : tr.j0;
+    prev_word = ld_u32(nj0 ? nbase - 4 : nbase);
+    // key 0 of a stream (local index 0 of lane 0 in tile 0) does not exist: i starts at 4
+    // (adapters.cpp:59).  Its packed values are zeroed, so it never becomes a lane's maximum.
+    const uint32_t key0_mask = (tr.j0 == 0 && lane == 0) ? 0u : ~0u;
+    uint32_t acc_first = 0, acc_last = 0, acc_grp = 0;
 #pragma unroll
     for (int it = 0; it < kTileIters; ++it) {
         // the 16 table addresses of this 16-byte slice; then the slot is free for the next
@@ -313,9 +346,22 @@ __device__ __forceinline__ void tile_scan(const TileRef &tr, const TileRef &nx,
         const uint32_t b3 = (e2 & 0xffff0000u) ^ (e3 << 16);
         // local key index l = 4*it + k;  "first" packs kLastLocal - l, "last" packs l
         const uint32_t inv = kLastLocal - 3u - 4u * it, idx = 4u * it;
-        acc_first = max3_u32(acc_first, b0 | inv | 3u, b1 | inv | 2u);
-        acc_first = max3_u32(acc_first, b2 | inv | 1u, b3 | inv);
-        acc_last = max3_u32(acc_last, b0 | idx, b1 | idx | 1u);
+        const uint32_t m0 = it == 0 ? key0_mask : ~0u;
+        if constexpr (G == 1) {
+            acc_first = max3_u32(acc_first, (b0 | inv | 3u) & m0, b1 | inv | 2u);
+            acc_first = max3_u32(acc_first, b2 | inv | 1u, b3 | inv);
+        } else {
+            acc_grp = max3_u32(acc_grp, (b0 | inv | 3u) & m0, b1 | inv | 2u);
+            acc_grp = max3_u32(acc_grp, b2 | inv | 1u, b3 | inv);
+            if ((it + 1) % kPer == 0) {  // compile-time after the unroll
+                const int g = it / kPer;
+                acc_first = max(acc_first, acc_grp);
+                if (g % 2 == 0) gpk[g / 2] = acc_grp >> 16;
+                else gpk[g / 2] |= acc_grp & 0xffff0000u;
+                acc_grp = 0;
+            }
+        }
+        acc_last = max3_u32(acc_last, (b0 | idx) & m0, b1 | idx | 1u);
         acc_last = max3_u32(acc_last, b2 | idx | 2u, b3 | idx | 3u);
     }
     top = acc_first >> 16;
@@ -333,6 +379,27 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
     const uint32_t r0 = __builtin_amdgcn_readlane(v, 15), r1 = __builtin_amdgcn_readlane(v, 31);
     const uint32_t r2 = __builtin_amdgcn_readlane(v, 47), r3 = __builtin_amdgcn_readlane(v, 63);
     return max(max(r0, r1), max(r2, r3));
+}
+
+__device__ __forceinline__ uint32_t pk_max_u16(uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_pk_max_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ uint32_t pk_max_u16_s(uint32_t a, uint32_t b) {  // uniform values
+    return max(a & 0xffffu, b & 0xffffu) | (max(a >> 16, b >> 16) << 16);
+}
+
+// Per-half maximum of two packed u16 values over the wave (uniform result): DPP row shifts,
+// then the four row maxima through readlane, as wave_max_u32.
+__device__ __forceinline__ uint32_t wave_max_pk16(uint32_t v) {
+    v = pk_max_u16(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false));
+    v = pk_max_u16(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false));
+    v = pk_max_u16(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false));
+    v = pk_max_u16(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false));
+    const uint32_t r0 = __builtin_amdgcn_readlane(v, 15), r1 = __builtin_amdgcn_readlane(v, 31);
+    const uint32_t r2 = __builtin_amdgcn_readlane(v, 47), r3 = __builtin_amdgcn_readlane(v, 63);
+    return pk_max_u16_s(pk_max_u16_s(r0, r1), pk_max_u16_s(r2, r3));
 }
 
 // Walks a wave's tile range across stream boundaries (all state wave-uniform).
@@ -360,8 +427,7 @@ struct TileCursor {
         TileRef r;
         r.base = sload_ptr(d.ptr + s);
         r.j0 = (t - cur) * kTileKeys;
-        r.fast = __builtin_amdgcn_readfirstlane(
-                     (uint32_t)(r.j0 >= kTileKeys && r.j0 + kTileKeys - 1 <= sload(d.jneed + s))) != 0;
+        r.fast = __builtin_amdgcn_readfirstlane((uint32_t)tile_fast(r.j0, sload(d.len + s))) != 0;
         return r;
     }
 };
@@ -394,10 +460,15 @@ __device__ __forceinline__ void stage_tile_tables(const KeyTables *tab) {
 }
 
 // Persistent: one 1024-thread workgroup per CU, each wave a contiguous range of tiles.
+// G > 1: also gmax[t] = the top-16 maximum of each of the tile's G key groups (u16 g at bits
+// 16g; keys that do not exist count as 0), an upper bound the chain uses to leave most of an
+// edge range unscanned (chain_step).
+template <int G>
 __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restrict__ tab,
                                                        StreamDesc d, uint64_t n_streams,
                                                        uint64_t n_tiles,
-                                                       TileRecord *__restrict__ rec) {
+                                                       TileRecord *__restrict__ rec,
+                                                       uint64_t *__restrict__ gmax) {
     stage_tile_tables(tab);
     const uint64_t *full = reinterpret_cast<const uint64_t *>(s_tile_lds + kFullOff / 4);
     const uint64_t *tl = full, *th = full + 1024;
@@ -417,7 +488,8 @@ __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restri
     while (!cur.fast && ++t < t_end) cur = cursor.at(t);
     if (!cur.fast) return;
     u32x4 x[kTileIters];
-    uint32_t prev_word = ld_u32(cur.base + 4 * cur.j0 - 4);
+    // the word before the first tile (tile 0 of a stream has none: key 0 is masked)
+    uint32_t prev_word = ld_u32(cur.base + 4 * cur.j0 - (cur.j0 ? 4 : 0));
     {
         const __amdgpu_buffer_rsrc_t src = tile_rsrc(cur.base + 4 * cur.j0);
 #pragma unroll
@@ -444,7 +516,14 @@ __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restri
             if (nx.fast) break;
         }
         uint32_t top, first, last;
-        tile_scan(cur, nx, x, prev_word, lb_a, lb_b, top, first, last);
+        uint32_t gpk[(G + 1) / 2];
+        tile_scan<G>(cur, nx, x, prev_word, lb_a, lb_b, top, first, last, gpk);
+        if constexpr (G > 1) {  // this tile's group maxima, stored now (no exact key needed)
+            uint64_t gm = 0;
+#pragma unroll
+            for (int i = 0; i < (G + 1) / 2; ++i) gm |= (uint64_t)wave_max_pk16(gpk[i]) << (32 * i);
+            if (lane == 0) gmax[t] = gm;
+        }
 
         // retire the pending tile: (first maximal exact key, index) over its candidate lanes
 #ifndef RC_DIAG_NO_TAIL
@@ -481,7 +560,7 @@ __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restri
         pend_mask = tie ? 0 : cmask;
         pend_jl = cand ? jl : win;  // non-candidates load the winner's (same) line
         const uint8_t *q = cur.base + 4 * (cur.j0 + pend_jl);
-        pend_lo = ld_u32(q - 4);
+        pend_lo = ld_u32(q - (cur.j0 + pend_jl ? 4 : 0));  // never key 0; no read before the stream
         pend_hi = ld_u32(q);
 #else
         if (lane == 0 && (top ^ first ^ last) == 0x5a5au) rec[t].key = first ^ last;  // keep the scan alive
@@ -523,25 +602,28 @@ __device__ __forceinline__ uint64_t stream_of_tile(const StreamDesc &d, uint64_t
 
 __device__ __forceinline__ void exact_tile(const uint64_t *tl, const uint64_t *th,
                                            const StreamDesc &d, uint64_t s, uint64_t t,
-                                           TileRecord *rec) {
+                                           TileRecord *rec, uint64_t *gmax) {
     const uint64_t j0 = (t - sload(d.tile_base + s)) * kTileKeys;
-    const uint64_t jb = min(j0 + kTileKeys - 1, sload(d.jneed + s));
+    const uint64_t jb = tile_key_end(j0, sload(d.len + s), sload(d.jneed + s));
     uint64_t bk = 0, bj = ~0ull;
     scan_ranges<kScanUnroll>(tl, th, sload_ptr(d.ptr + s), max(j0, (uint64_t)1), jb, 1, 0, bk, bj);
     wave_best(bk, bj);
     if (lane_id() == 0) {
         rec[t].key = bk;
         rec[t].j = bj;
+        if (gmax) gmax[t] = ~0ull;  // no group bounds for an exact tile: the chain scans
     }
 }
 
-// Exact tiles, one wave per item, grid-strided: items 0 .. 2n-1 are tile 0 and a partial
-// last tile of every stream; the rest sweep the records in 64-record chunks for the tiles the
-// fast kernel marked (kTieMark) and recompute those.
+// Exact tiles, one wave per item, grid-strided: items 0 .. 2n-1 are tile 0 and the last tile
+// of every stream when the fast kernel could not take them (tile_fast: the stream ends inside
+// the tile); the rest sweep the records in 64-record chunks for the tiles the fast kernel
+// marked (kTieMark) and recompute those over the same key range (tile_key_end).
 __global__ __launch_bounds__(256) void rc_edge_kernel(const KeyTables *__restrict__ tab,
                                                       StreamDesc d, uint64_t n_streams,
                                                       uint64_t n_tiles,
-                                                      TileRecord *__restrict__ rec) {
+                                                      TileRecord *__restrict__ rec,
+                                                      uint64_t *__restrict__ gmax) {
     __shared__ __attribute__((aligned(16))) uint64_t s_full[2048];
     const uint64_t *gfull = &tab->tl[0][0];
     for (uint32_t i = threadIdx.x; i < 2048u; i += blockDim.x) s_full[i] = gfull[i];
@@ -557,18 +639,18 @@ __global__ __launch_bounds__(256) void rc_edge_kernel(const KeyTables *__restric
             const uint64_t tb = sload(d.tile_base + s), nt = sload(d.tile_base + s + 1) - tb;
             if (nt == 0) continue;
             uint64_t t = tb;
-            if (e & 1) {  // the last tile, unless it is tile 0 or a full (fast) tile
+            if (e & 1) {  // the last tile, unless it is tile 0
                 if (nt < 2) continue;
-                if ((nt - 1) * kTileKeys + kTileKeys - 1 <= sload(d.jneed + s)) continue;
                 t = tb + nt - 1;
             }
-            exact_tile(tl, th, d, s, t, rec);
+            if (tile_fast((t - tb) * kTileKeys, sload(d.len + s))) continue;
+            exact_tile(tl, th, d, s, t, rec, gmax);
         } else {
             const uint64_t t0 = (e - 2 * n_streams) * 64, t = t0 + lane_id();
             const bool marked = t < n_tiles && rec[t].j == kTieMark;
             for (uint64_t m = __ballot(marked); m; m &= m - 1) {
                 const uint64_t tm = t0 + __builtin_ctzll(m);
-                exact_tile(tl, th, d, stream_of_tile(d, n_streams, tm), tm, rec);
+                exact_tile(tl, th, d, stream_of_tile(d, n_streams, tm), tm, rec, gmax);
             }
         }
     }
@@ -587,7 +669,7 @@ __global__ __launch_bounds__(256) void rc_edge_kernel(const KeyTables *__restric
 
 struct ChainStream {
     const uint8_t *base;
-    uint64_t L, P, tb0, jmax;
+    uint64_t L, P, tb0, nt, jmax;
 #ifdef RC_DIAG_STAMPS
     bool diag;
 #endif
@@ -599,6 +681,7 @@ __device__ __forceinline__ ChainStream chain_stream(const StreamDesc &d, uint64_
     st.L = sload(d.len + s);
     st.P = sload(d.last + s);
     st.tb0 = sload(d.tile_base + s);
+    st.nt = sload(d.tile_base + s + 1) - st.tb0;
     st.jmax = st.L >= 8 ? (st.L - 4) / 4 : 0;
 #ifdef RC_DIAG_STAMPS
     st.diag = s == 0;
@@ -723,6 +806,78 @@ struct EdgeRange {
 
 enum : int { kStepStop = 0, kStepCut = 1, kStepTail1 = 2, kStepTail2 = 3 };
 
+// Trim the key range [a, b] inside tile `te` to the groups whose top-16 maximum (gm: u16 per
+// group) reaches tb16; an empty result becomes a > b.  Returns whether the range changed.
+__device__ __forceinline__ bool trim_groups(uint64_t gm, uint64_t te, uint32_t tb16, uint64_t &a,
+                                            uint64_t &b) {
+    const uint64_t tj0 = te * kTileKeys;
+    uint32_t ga = (uint32_t)((a - tj0) / kGroupKeys), gb = (uint32_t)((b - tj0) / kGroupKeys);
+    const uint32_t ga0 = ga, gb0 = gb;
+    while (ga <= gb && ((gm >> (16 * ga)) & 0xffffu) < tb16) ++ga;
+    while (gb > ga && ((gm >> (16 * gb)) & 0xffffu) < tb16) --gb;
+    if (ga > gb) {
+        a = 1;
+        b = 0;
+        return true;
+    }
+    if (ga == ga0 && gb == gb0) return false;
+    a = max(a, tj0 + (uint64_t)ga * kGroupKeys);
+    b = min(b, tj0 + (uint64_t)(gb + 1) * kGroupKeys - 1);
+    return true;
+}
+
+// A walker's window onto its stream's tile records, held in registers across chain steps:
+// lane l of row u holds the record of stream tile c0 + 64u + l.  Consecutive windows overlap
+// (a chunk advances by less than a window), so while the next step's tiles lie inside the
+// cached span the step reads no memory at all for its records -- with windows of a few tiles
+// (small max_length) a whole stream of up to 64R tiles is loaded once.  A step that needs
+// tiles outside it reloads the span from its first needed tile (one round trip, as before).
+template <int R>
+struct RecCache {
+    uint64_t c0 = 0, n = 0;  // cached stream tiles [c0, c0 + n)
+    TileRecord v[R];
+    uint64_t g[R];           // group maxima of the same tiles (when the tile kernel made them)
+
+    __device__ bool has(uint64_t t) const { return t >= c0 && t - c0 < n; }
+    __device__ void load(const TileRecord *rec, const uint64_t *gmax, const ChainStream &st,
+                         uint64_t lo) {
+        c0 = lo;
+        n = min(st.nt - lo, (uint64_t)64 * R);
+        const uint64_t lane = lane_id();
+#pragma unroll
+        for (int u = 0; u < R; ++u)
+            if ((uint64_t)64 * u < n) {
+                const uint64_t t = st.tb0 + lo + min((uint64_t)64 * u + lane, n - 1);
+                v[u] = rec[t];
+                if (gmax) g[u] = gmax[t];
+            }
+    }
+    __device__ TileRecord get(uint64_t t, uint64_t &gm) const {  // t uniform and cached
+        const uint64_t off = t - c0;
+        const int row = (int)(off >> 6), l = (int)(off & 63);
+        TileRecord r = {0, 0};
+        gm = ~0ull;
+#pragma unroll
+        for (int u = 0; u < R; ++u)
+            if (u == row) {
+                r.key = lane_u64(v[u].key, l);
+                r.j = lane_u64(v[u].j, l);
+                gm = lane_u64(g[u], l);
+            }
+        return r;
+    }
+    // (key desc, index asc) best of the cached records of tiles [t_lo, t_hi), per lane
+    __device__ void reduce(uint64_t t_lo, uint64_t t_hi, uint64_t &bk, uint64_t &bj) const {
+        const uint64_t lane = lane_id();
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+            const uint64_t t = c0 + 64 * u + lane;
+            if ((uint64_t)64 * u < n && t - c0 < n && t >= t_lo && t < t_hi && v[u].key != 0)
+                take_best(v[u].key, v[u].j, bk, bj);
+        }
+    }
+};
+
 #ifdef RC_DIAG_STAMPS
 // diagnostic build only: per-step s_memrealtime stamps (100 MHz) of stream 0's walker
 __device__ uint64_t g_diag[4096];
@@ -742,10 +897,11 @@ __device__ uint32_t g_diag_n;
 // One chain step from chunk start `pos` (< L): an argmax cut (adapters.cpp:59-69), or the tail
 // rule's one or two final cuts (adapters.cpp:48-55), or stop (non-final wait / S7 UB).
 // prm.max_steps == 0 is the raw single next_cut: c1 = the argmax offset, whatever its value.
-template <bool kCompact>
+template <int R>
 __device__ int chain_step(const uint64_t *tl, const uint64_t *th, const uint32_t *pf,
                           const TileRecord *rec, const ChainStream &st, const ChainParams &prm,
-                          uint64_t pos, uint32_t lb_a, uint32_t lb_b, uint64_t &c1, uint64_t &c2) {
+                          RecCache<R> &cache, uint64_t pos, uint32_t lb_a, uint32_t lb_b,
+                          uint64_t &c1, uint64_t &c2) {
     const uint64_t minl = prm.min_length, maxl = prm.max_length, T = prm.window;
     const bool single = prm.max_steps == 0;
     const uint64_t rem = st.L - pos;
@@ -776,31 +932,49 @@ __device__ int chain_step(const uint64_t *tl, const uint64_t *th, const uint32_t
             r1.init(st.base, st.L / 4 - 1, a1, b1, 1);
             uint32_t w0[kEdgeIters][4], w1[kEdgeIters][4];
             uint32_t acc_first = 0, acc_last = 0;
-            TileRecord rv[kRecUnroll];
-            const uint64_t rlo = st.tb0 + t_lo, rhi = st.tb0 + t_hi;
-            // only as many 64-record rows as the window has tiles (one for max_length up to
-            // 512 KiB; a default window has 625 tiles and takes all kRecUnroll and the loop)
-            const uint64_t nrow = have_rec ? min((rhi - rlo + 63) / 64, (uint64_t)kRecUnroll) : 0;
-#pragma unroll
-            for (int u = 0; u < kRecUnroll; ++u)
-                if ((uint64_t)u < nrow) rv[u] = rec[min(rlo + 64 * u + lane_id(), rhi - 1)];
             // An edge range inside one tile needs no scan when that tile's record -- its FIRST
             // maximal key -- lies in the range (the first maximum of a set is the first maximum
             // of every subset holding it), or when the tile's keys are all 0 (never taken,
-            // adapters.cpp:60-63).  These records come with the window's, in one round trip.
+            // adapters.cpp:60-63).
             const bool one0 = r0.live && a0 / kTileKeys == b0 / kTileKeys;
             const bool one1 = r1.live && a1 / kTileKeys == b1 / kTileKeys;
-            TileRecord er0 = {}, er1 = {};
-            if (one0) er0 = rec[st.tb0 + a0 / kTileKeys];
-            if (one1) er1 = rec[st.tb0 + a1 / kTileKeys];
+            const uint64_t te0 = a0 / kTileKeys, te1 = a1 / kTileKeys;
+            // the tiles this step reads records of: the window's full tiles and the edge tiles
+            uint64_t need_lo = ~0ull, need_hi = 0;
             if (have_rec) {
-#pragma unroll
-                for (int u = 0; u < kRecUnroll; ++u)
-                    if ((uint64_t)u < nrow && rlo + 64 * u + lane_id() < rhi && rv[u].key != 0)
-                        take_best(rv[u].key, rv[u].j, bk, bj);
-                if (rhi - rlo > 64 * kRecUnroll)  // windows beyond 512 tiles (max > 8 MiB)
-                    scan_records(rec, rlo + 64 * kRecUnroll, rhi, bk, bj);
+                need_lo = t_lo;
+                need_hi = t_hi - 1;
             }
+            if (one0) {
+                need_lo = min(need_lo, te0);
+                need_hi = max(need_hi, te0);
+            }
+            if (one1) {
+                need_lo = min(need_lo, te1);
+                need_hi = max(need_hi, te1);
+            }
+            if (need_lo <= need_hi && !(cache.has(need_lo) && cache.has(need_hi)))
+                cache.load(rec, prm.gmax, st, need_lo);  // one round trip, edge records included
+            // edge tiles past the span (windows wider than 64R tiles) come from memory, issued
+            // together with the reload
+            TileRecord er0 = {}, er1 = {};
+            uint64_t gm0 = ~0ull, gm1 = ~0ull;
+            const bool g0 = one0 && !cache.has(te0), g1 = one1 && !cache.has(te1);
+            if (g0) {
+                er0 = rec[st.tb0 + te0];
+                if (prm.gmax) gm0 = prm.gmax[st.tb0 + te0];
+            }
+            if (g1) {
+                er1 = rec[st.tb0 + te1];
+                if (prm.gmax) gm1 = prm.gmax[st.tb0 + te1];
+            }
+            if (have_rec) {
+                cache.reduce(t_lo, t_hi, bk, bj);
+                if (t_hi > cache.c0 + cache.n)  // a window wider than the span
+                    scan_records(rec, st.tb0 + max(cache.c0 + cache.n, t_lo), st.tb0 + t_hi, bk, bj);
+            }
+            if (one0 && !g0) er0 = cache.get(te0, gm0);
+            if (one1 && !g1) er1 = cache.get(te1, gm1);
             wave_best(bk, bj);
             // Otherwise the record still bounds the range from above: the head range (indices
             // below every full tile's) cannot win when its bound is below the records' best,
@@ -814,6 +988,18 @@ __device__ int chain_step(const uint64_t *tl, const uint64_t *th, const uint32_t
                 if (er1.key != 0 && er1.j >= a1 && er1.j <= b1) take_best(er1.key, er1.j, bk, bj);
                 r1.live = false;
             }
+            // With group maxima (small windows): a key group whose top-16 maximum is below bk's
+            // top 16 bits holds no key >= bk, so it cannot win, head or tail; the range left to
+            // scan is trimmed to its groups from the first to the last one that can.  The head
+            // tile always holds the previous cut's key -- the maximum of the previous window --
+            // so its record rarely settles the head; its groups after that key usually do.
+            if (prm.gmax) {
+                const uint32_t tb16 = (uint32_t)(bk >> 48);
+                if (one0 && r0.live && trim_groups(gm0, te0, tb16, a0, b0))
+                    r0.init(st.base, st.L / 4 - 1, a0, b0, 0);
+                if (one1 && r1.live && trim_groups(gm1, te1, tb16, a1, b1))
+                    r1.init(st.base, st.L / 4 - 1, a1, b1, 1);
+            }
             // the few ranges left are scanned: their first batches only now (a second round
             // trip for them; none at all for the rest)
             if (r0.more()) r0.load(w0);
@@ -825,11 +1011,11 @@ __device__ int chain_step(const uint64_t *tl, const uint64_t *th, const uint32_t
                 const bool m0 = r0.more(), m1 = r1.more();
                 if (!m0 && !m1) break;
                 if (m0) {
-                    r0.template compute<kCompact>(w0, lb_a, lb_b, pf, acc_first, acc_last);
+                    r0.template compute<true>(w0, lb_a, lb_b, pf, acc_first, acc_last);
                     if (r0.more()) r0.load(w0);
                 }
                 if (m1) {
-                    r1.template compute<kCompact>(w1, lb_a, lb_b, pf, acc_first, acc_last);
+                    r1.template compute<true>(w1, lb_a, lb_b, pf, acc_first, acc_last);
                     if (r1.more()) r1.load(w1);
                 }
             }
@@ -897,12 +1083,11 @@ __device__ __forceinline__ uint64_t find_index(const uint64_t *base_arr, uint64_
 // Spec kernel: one wave per segment.  A one-segment stream writes its final cuts directly;
 // segment i of a longer stream writes its list to the scratch and its count (bit 63 set if the
 // chain ended inside the list: tail rule or stop).
-#ifndef RC_SPEC_WAVES
-#define RC_SPEC_WAVES 4
-#endif
-constexpr int kSpecWaves = RC_SPEC_WAVES;  // waves per workgroup (20 KiB LDS: ~6 groups per CU)
-
-__global__ __launch_bounds__(kSpecWaves * 64) void rc_spec_kernel(const KeyTables *__restrict__ tab,
+// Workgroups of kChainWaves walkers on 20 KiB of LDS.  R = rows of the record cache: 1 for
+// windows of up to ~60 tiles (max_length below ~1 MB: a 1 MiB stream's records load once),
+// 4 otherwise (a default window spans 313 tiles and reloads every step, as it must).
+template <int R>
+__global__ __launch_bounds__(kChainWaves * 64) void rc_spec_kernel(const KeyTables *__restrict__ tab,
                                                       StreamDesc d, uint64_t n_streams,
                                                       ChainParams prm, uint64_t n_segs,
                                                       const TileRecord *__restrict__ rec,
@@ -931,6 +1116,7 @@ __global__ __launch_bounds__(kSpecWaves * 64) void rc_spec_kernel(const KeyTable
 
     uint64_t pos = i * prm.seg_bytes, n = 0, ext = 0;
     bool overflow = false, term = false;
+    RecCache<R> cache;
     auto emit = [&](uint64_t c) {
         if (n >= cap) {
             overflow = true;
@@ -946,7 +1132,7 @@ __global__ __launch_bounds__(kSpecWaves * 64) void rc_spec_kernel(const KeyTable
         }
         if (!direct && pos >= seg_end && ext++ >= prm.ext_steps) break;
         uint64_t c1 = 0, c2 = 0;
-        const int kind = chain_step<true>(tl, th, pf, rec, st, prm, pos, lb_a, lb_b, c1, c2);
+        const int kind = chain_step<R>(tl, th, pf, rec, st, prm, cache, pos, lb_a, lb_b, c1, c2);
         if (kind == kStepStop) {
             term = true;
             break;
@@ -1115,6 +1301,7 @@ __global__ __launch_bounds__(256) void rc_mark_kernel(StreamDesc d, uint64_t n_s
 
 // Join kernel: one wave per multi-segment stream, following the true chain across the
 // speculative lists (see above).  Only streams the scan marked kNeedJoin.
+template <int R>
 __global__ __launch_bounds__(256) void rc_join_kernel(const KeyTables *__restrict__ tab,
                                                       StreamDesc d, uint64_t n_streams,
                                                       ChainParams prm,
@@ -1151,6 +1338,7 @@ __global__ __launch_bounds__(256) void rc_join_kernel(const KeyTables *__restric
 
     uint64_t pos = 0, n = 0, src = 0, idx = 0;
     bool overflow = false, src_term, bad;
+    RecCache<R> cache;
     uint64_t src_cnt = count_of(0, src_term, bad);
     overflow |= bad;
     while (!overflow) {
@@ -1225,7 +1413,7 @@ __global__ __launch_bounds__(256) void rc_join_kernel(const KeyTables *__restric
         }
         if (pos >= st.L) break;
         uint64_t c1 = 0, c2 = 0;
-        const int kind = chain_step<true>(tl, th, pf, rec, st, prm, pos, lb_a, lb_b, c1, c2);
+        const int kind = chain_step<R>(tl, th, pf, rec, st, prm, cache, pos, lb_a, lb_b, c1, c2);
         if (kind == kStepStop) break;
         if (n + (kind == kStepTail2 ? 2 : 1) > cap) {
             overflow = true;
@@ -1295,6 +1483,20 @@ __global__ void rc_fill_kernel(uint8_t *__restrict__ dst, uint64_t nbytes, uint6
     }
 }
 
+// n streams of nbytes each, `slot` bytes apart (slot % 8 == 0, slot >= nbytes rounded up to 8:
+// a stream's last word is written whole, into its slot's slack), stream k has id id0 + k*id_step
+__global__ void rc_fill_streams_kernel(uint8_t *__restrict__ dst, uint64_t n, uint64_t nbytes,
+                                       uint64_t slot, uint64_t seed, uint64_t id0,
+                                       uint64_t id_step) {
+    const uint64_t wps = (nbytes + 7) / 8, total = n * wps;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+        const uint64_t k = i / wps, w = i - k * wps;
+        const uint64_t base = (seed * 0x9E3779B97F4A7C15ull) ^ ((id0 + k * id_step) << 34);
+        reinterpret_cast<uint64_t *>(dst + k * slot)[w] = splitmix64(base ^ w);
+    }
+}
+
 int launch_status(const char *what) {
     const hipError_t e = hipGetLastError();
     if (e == hipSuccess) return 0;
@@ -1335,22 +1537,34 @@ int rc_diag_read(uint64_t *out, uint32_t cap, uint32_t *n) {
 #endif
 
 int rc_launch_tiles(const KeyTables *d_tables, StreamDesc desc, uint64_t n_streams,
-                    uint64_t n_tiles, TileRecord *d_records, void *stream) {
-    if (n_tiles == 0) return 0;
+                    uint64_t n_tiles, TileRecord *d_records, uint64_t *d_gmax, void *stream,
+                    void *mid_event) {
     hipStream_t st = (hipStream_t)stream;
+    if (n_tiles == 0) {
+        if (mid_event && hipEventRecord((hipEvent_t)mid_event, st) != hipSuccess) return 1;
+        return 0;
+    }
     const uint64_t waves_per_wg = 1024 / kWaveSize;
     uint64_t grid = (n_tiles + waves_per_wg - 1) / waves_per_wg;
     const uint64_t cus = (uint64_t)cu_count();
     if (grid > cus) grid = cus;  // persistent: one 144 KiB-LDS workgroup per CU
-    hipLaunchKernelGGL(rc_tile_kernel, dim3((unsigned)grid), dim3(1024), 0, st, d_tables, desc,
-                       n_streams, n_tiles, d_records);
+    if (d_gmax)
+        hipLaunchKernelGGL(rc_tile_kernel<kTileGroups>, dim3((unsigned)grid), dim3(1024), 0, st,
+                           d_tables, desc, n_streams, n_tiles, d_records, d_gmax);
+    else
+        hipLaunchKernelGGL(rc_tile_kernel<1>, dim3((unsigned)grid), dim3(1024), 0, st, d_tables,
+                           desc, n_streams, n_tiles, d_records, d_gmax);
     if (launch_status("rc_tile_kernel")) return 1;
+    if (mid_event && hipEventRecord((hipEvent_t)mid_event, st) != hipSuccess) {
+        snprintf(g_launch_err, sizeof g_launch_err, "hipEventRecord failed");
+        return 1;
+    }
     // edge tiles (2 per stream) + the marked-tile sweep (64 records per item), one wave each
     uint64_t egrid = (2 * n_streams + (n_tiles + 63) / 64 + 3) / 4;
     if (egrid > 4 * cus) egrid = 4 * cus;
     if (egrid == 0) egrid = 1;
     hipLaunchKernelGGL(rc_edge_kernel, dim3((unsigned)egrid), dim3(256), 0, st, d_tables, desc,
-                       n_streams, n_tiles, d_records);
+                       n_streams, n_tiles, d_records, d_gmax);
     return launch_status("rc_edge_kernel");
 }
 
@@ -1360,12 +1574,17 @@ int rc_launch_chain(const KeyTables *d_tables, StreamDesc desc, uint64_t n_strea
                     uint64_t *d_seg_counts, bool any_multi, void *stream) {
     if (n_streams == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
-    // 4-wave workgroups on 20 KiB of LDS (compact tables): about 6 per CU
-    const uint64_t wpg = n_segs >= kSpecWaves * (uint64_t)cu_count() ? kSpecWaves : kChainWaves;
-    const uint64_t grid = (n_segs + wpg - 1) / wpg;
-    hipLaunchKernelGGL(rc_spec_kernel, dim3((unsigned)grid), dim3(wpg * kWaveSize), 0, st,
-                       d_tables, desc, n_streams, prm, n_segs, d_records, d_cuts, d_counts,
-                       d_scratch, d_seg_counts);
+    // 4-wave workgroups on 20 KiB of LDS (compact tables)
+    const bool small = prm.window / kTileKeys + 3 <= 64;  // window + both edge tiles in one row
+    const uint64_t grid = (n_segs + kChainWaves - 1) / kChainWaves;
+    if (small)
+        hipLaunchKernelGGL(rc_spec_kernel<1>, dim3((unsigned)grid), dim3(kChainWaves * kWaveSize),
+                           0, st, d_tables, desc, n_streams, prm, n_segs, d_records, d_cuts,
+                           d_counts, d_scratch, d_seg_counts);
+    else
+        hipLaunchKernelGGL(rc_spec_kernel<kRecUnroll>, dim3((unsigned)grid),
+                           dim3(kChainWaves * kWaveSize), 0, st, d_tables, desc, n_streams, prm,
+                           n_segs, d_records, d_cuts, d_counts, d_scratch, d_seg_counts);
     if (launch_status("rc_spec_kernel")) return 1;
     if (!any_multi) return 0;
     // d_seg_counts holds 4 arrays of n_segs: counts, merge points, slice offsets, slices
@@ -1391,9 +1610,15 @@ int rc_launch_chain(const KeyTables *d_tables, StreamDesc desc, uint64_t n_strea
                            st, desc, n_streams, d_counts);
         if (launch_status("rc_mark_kernel")) return 1;
     }
-    hipLaunchKernelGGL(rc_join_kernel, dim3((unsigned)jgrid), dim3(kChainWaves * kWaveSize), 0, st,
-                       d_tables, desc, n_streams, prm, d_records, d_cuts, d_counts,
-                       (const uint64_t *)d_scratch, (const uint64_t *)d_seg_counts);
+    if (small)
+        hipLaunchKernelGGL(rc_join_kernel<1>, dim3((unsigned)jgrid), dim3(kChainWaves * kWaveSize),
+                           0, st, d_tables, desc, n_streams, prm, d_records, d_cuts, d_counts,
+                           (const uint64_t *)d_scratch, (const uint64_t *)d_seg_counts);
+    else
+        hipLaunchKernelGGL(rc_join_kernel<kRecUnroll>, dim3((unsigned)jgrid),
+                           dim3(kChainWaves * kWaveSize), 0, st, d_tables, desc, n_streams, prm,
+                           d_records, d_cuts, d_counts, (const uint64_t *)d_scratch,
+                           (const uint64_t *)d_seg_counts);
     return launch_status("rc_join_kernel");
 }
 
@@ -1406,6 +1631,17 @@ int rc_launch_read_probe(const uint8_t *d_src, uint64_t nbytes, uint32_t *d_out,
     hipLaunchKernelGGL(rc_read_probe_kernel, dim3((unsigned)grid), dim3(1024), 0,
                        (hipStream_t)stream, d_src, n_tiles, d_out);
     return launch_status("rc_read_probe_kernel");
+}
+
+int rc_launch_fill_streams(uint8_t *d_dst, uint64_t n, uint64_t nbytes, uint64_t slot,
+                           uint64_t seed, uint64_t id0, uint64_t id_step, void *stream) {
+    if (n == 0 || nbytes == 0) return 0;
+    const uint64_t words = n * ((nbytes + 7) / 8);
+    uint64_t grid = (words + 255) / 256;
+    if (grid > 65536) grid = 65536;
+    hipLaunchKernelGGL(rc_fill_streams_kernel, dim3((unsigned)grid), dim3(256), 0,
+                       (hipStream_t)stream, d_dst, n, nbytes, slot, seed, id0, id_step);
+    return launch_status("rc_fill_streams_kernel");
 }
 
 int rc_launch_fill(uint8_t *d_dst, uint64_t nbytes, uint64_t seed, uint64_t stream_id,

@@ -45,6 +45,29 @@ def seeded_key(seed: int) -> bytes:
     return w.astype('<u8').tobytes()
 
 
+# ------------------------------------------- the reference's own benchmark stream (harness)
+
+HARNESS_NUMBER = 10          # repository.py:1984 _benchmark_chunker(number=10, ...)
+HARNESS_SIZE = 512_000_000   # ... size=512_000_000
+HARNESS_PIECE = 16_777_216   # repository.py:1992 method(16_777_216)
+
+
+def harness_buffers(number: int = HARNESS_NUMBER, size: int = HARNESS_SIZE, seed: int = 0):
+    """The pieces ``Repository._benchmark_chunker`` feeds the chunker adapter
+    (/root/reference/replicat/repository.py:1984-1999): one ``random.Random(seed)`` (what
+    ``replicat.utils.compat.Random`` is on Python >= 3.9), and per piece 16 MiB ``randbytes``
+    appended until ``size`` bytes, the excess dropped.  Each piece is one adapter piece, so the
+    stream is ``number * size`` bytes whose last piece starts at ``(number - 1) * size``."""
+    import random
+    method = random.Random(seed).randbytes
+    for _ in range(number):
+        buf = bytearray()
+        while len(buf) < size:
+            buf += method(HARNESS_PIECE)
+        del buf[size:]
+        yield buf
+
+
 # ------------------------------------------------------------------ config 5: edited copies
 
 EDIT_KINDS = ('overwrite1', 'insert4', 'insert1')

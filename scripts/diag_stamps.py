@@ -9,7 +9,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from replicat_amd import _lib, synth  # noqa: E402
-from replicat_amd.chunker import GpuChunker, fill_splitmix  # noqa: E402
+from replicat_amd.chunker import GpuChunker, fill_splitmix_streams  # noqa: E402
 
 # usage: diag_stamps.py [n_streams] [stream_mib] [min] [max]   (default: config 2)
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
@@ -20,8 +20,7 @@ ch = GpuChunker(mn, mx, b'\xff' * 16)
 pool = torch.empty(n * size, dtype=torch.uint8, device='cuda')
 ptrs = [pool.data_ptr() + i * size for i in range(n)]
 hs = torch.cuda.current_stream().cuda_stream
-for i, p in enumerate(ptrs):
-    fill_splitmix(p, size, synth.DEFAULT_SEED, i, hs)
+fill_splitmix_streams(pool.data_ptr(), n, size, size, synth.DEFAULT_SEED, 0, 1, hs)
 total, caps = ch.capacity([size] * n)
 cuts = torch.zeros(total, dtype=torch.int64, device='cuda')
 counts = torch.zeros(n, dtype=torch.int64, device='cuda')

@@ -355,6 +355,91 @@ def make_config5(pool, n_streams=1024, n_edit=512, size=64 << 20):
             'dedup_ratio_set': (dup + unedited) / (total + unedited)}
 
 
+# ----------------------------------------------------- config 4: 128 x 8 GiB (config4.json)
+
+C4_STREAMS, C4_SIZE, C4_GPUS = 128, 8 << 30, 8
+
+
+def _config4_job(sid):
+    """One 8 GiB stream of config 4, one piece (P = 0), cut by the REFERENCE's native
+    ``next_cut`` exactly as its adapter cuts a single piece (adapters.py:290-305: every call is
+    final, the buffer is the uncut rest) -- on a zero-copy view instead of the adapter's
+    bytearray, whose copy of an 8 GiB piece would double the memory.  The bytes come from the
+    oracle's C splitmix filler (the same bytes as synth.stream_bytes and rc_fill_splitmix)."""
+    import numpy as np
+    from oracle import oracle as o
+    data = np.empty(C4_SIZE, dtype=np.uint8)
+    o.lib().oc_fill_splitmix(data.ctypes.data, C4_SIZE, synth.DEFAULT_SEED, sid)
+    ch = REF_EXT._gclmulchunker(MIN_DEF, MAX_DEF, b'\xff' * 16)
+    mv = memoryview(data)
+    pos, ends = 0, []
+    while pos < C4_SIZE:
+        c = ch.next_cut(mv[pos:], True)
+        if not c:
+            break
+        pos += c
+        ends.append(pos)
+    del mv, data
+    return sid, ends
+
+
+def _config4_adapter_check(sid=0, piece=16 << 20):
+    """Stream ``sid`` through replicat's adapter itself, fed 16 MiB pieces: P = L - 16 MiB,
+    which for L - P >= max cuts exactly like the single piece."""
+    base = synth.stream_base(synth.DEFAULT_SEED, sid)
+
+    def pieces():
+        for off in range(0, C4_SIZE, piece):
+            yield synth.splitmix_words(base, off // 8, piece // 8).view('<u1').tobytes()
+    return _ref_ends(MIN_DEF, MAX_DEF, pieces())
+
+
+def make_config4(procs=4):
+    """Config 4 (SURVEY §8 d): 128 streams x 8 GiB, stream i on GPU i mod 8, one piece each.
+    Per-stream cut-list SHA-256 (+ first/last ends) and, per GPU, the digest over its 16
+    streams in shard order (bench.shard_ids('4', g, 16) = g, g + 8, ...)."""
+    with mp.get_context('fork').Pool(procs) as pool:
+        chk = pool.apply_async(_config4_adapter_check)
+        res = dict(pool.imap_unordered(_config4_job, range(C4_STREAMS)))
+        adapter_ends = chk.get()
+    assert adapter_ends == res[0], 'adapter over 16 MiB pieces disagrees with one piece'
+    streams = [{'id': i, 'chunks': len(res[i]), 'sha256': cutlist_digest([res[i]]),
+                'first_ends': res[i][:8], 'last_ends': res[i][-8:]} for i in range(C4_STREAMS)]
+    per_gpu = []
+    for g in range(C4_GPUS):
+        ids = [g + C4_GPUS * k for k in range(C4_STREAMS // C4_GPUS)]
+        per_gpu.append({'gpu': g, 'ids': ids, 'chunks': sum(len(res[i]) for i in ids),
+                        'sha256': cutlist_digest([res[i] for i in ids])})
+    return {'name': 'config4', 'streams': C4_STREAMS, 'size': C4_SIZE, 'gpus': C4_GPUS,
+            'seed': synth.DEFAULT_SEED, 'min': MIN_DEF, 'max': MAX_DEF, 'params': None,
+            'last_piece': 0, 'adapter_checked_stream': 0, 'per_stream': streams,
+            'per_gpu': per_gpu}
+
+
+# ------------------------------------- the reference's benchmark harness (harness.json)
+
+def make_harness():
+    """Cut list of ``Repository._benchmark_chunker``'s stream (repository.py:1984-2008): 10 x
+    512,000,000-byte Random(0) pieces through replicat's adapter over its own extension."""
+    ends = _ref_ends(MIN_DEF, MAX_DEF, synth.harness_buffers())
+    n, size = synth.HARNESS_NUMBER, synth.HARNESS_SIZE
+    return {'name': 'harness', 'number': n, 'size': size, 'seed': 0, 'length': n * size,
+            'last_piece': (n - 1) * size, 'min': MIN_DEF, 'max': MAX_DEF, 'params': None,
+            'chunks': len(ends), 'sha256': cutlist_digest([ends]), 'first_ends': ends[:16],
+            'last_ends': ends[-16:]}
+
+
+def make_config3iii_full(pool):
+    """Config 3 (iii) in full: 65,536 x 1 MiB, min 2,000 / max 80,000 (digests.json keeps the
+    first 4,096 too)."""
+    jobs = [('splitmix', (synth.DEFAULT_SEED, i, 1 << 20, 0, 2_000, 80_000, None))
+            for i in range(65536)]
+    ends = pool.map(_stream_job, jobs, chunksize=64)
+    return {'name': 'config3iii', 'streams': 65536, 'size': 1 << 20, 'seed': synth.DEFAULT_SEED,
+            'min': 2_000, 'max': 80_000, 'params': None, 'chunks': sum(map(len, ends)),
+            'sha256': cutlist_digest(ends)}
+
+
 # ------------------------------------------------------------- module surface
 
 from golden_surface import SURFACE_CASES, surface_call  # noqa: E402
@@ -418,6 +503,31 @@ def make_snapshots():
 
 def main():
     quick = '--quick' in sys.argv
+    if '--harness' in sys.argv:
+        h = make_harness()
+        print('harness', h['chunks'], h['sha256'], flush=True)
+        with open(os.path.join(HERE, 'harness.json'), 'w') as f:
+            json.dump(h, f, separators=(',', ':'))
+            f.write('\n')
+        return
+    if '--config3iii' in sys.argv:
+        with mp.get_context('fork').Pool(8) as pool:
+            d = make_config3iii_full(pool)
+        print('config3iii', d['chunks'], d['sha256'], flush=True)
+        path = os.path.join(HERE, 'digests.json')
+        with open(path) as f:
+            sets = [s for s in json.load(f) if s['name'] != 'config3iii']
+        with open(path, 'w') as f:
+            json.dump(sets + [d], f, separators=(',', ':'))
+            f.write('\n')
+        return
+    if '--config4' in sys.argv:
+        c4 = make_config4()
+        print('config4', [g['sha256'][:16] for g in c4['per_gpu']], flush=True)
+        with open(os.path.join(HERE, 'config4.json'), 'w') as f:
+            json.dump(c4, f, separators=(',', ':'))
+            f.write('\n')
+        return
     if '--large' in sys.argv:
         with mp.get_context('fork').Pool(8) as pool:
             r3 = pool.apply_async(make_config3ii)

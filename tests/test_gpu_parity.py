@@ -232,9 +232,11 @@ def test_host_path_matches_device():
         assert g.tolist() == o.chunk_stream(b, 128_000, 5_120_000, None, 0)
 
 
-@pytest.mark.parametrize('kind', ['random', 'zeros', 'periodic', 'seeded_key'])
+@pytest.mark.parametrize('kind', ['random', 'zeros', 'periodic', 'seeded_key', 'framed'])
 def test_tile_records_vs_oracle(kind):
-    """Phase A alone: every tile record (first maximal exact key, index) equals the oracle's."""
+    """Phase A alone: every tile record (first maximal exact key, index) equals the oracle's.
+    'framed': last pieces near the stream end put jneed within a tile of the last key, so the
+    last tile runs past the data and takes the edge kernel (the others take the fast path)."""
     import ctypes
     o = _oracle()
     from replicat_amd.chunker import keys_needed, tile_keys
@@ -250,24 +252,67 @@ def test_tile_records_vs_oracle(kind):
         datas = [np.resize(rnd.integers(0, 256, 4096 + 12, dtype=np.uint8), n) for n in sizes]
     else:
         datas = [synth.stream_bytes(n, synth.DEFAULT_SEED, 100 + i) for i, n in enumerate(sizes)]
+    last = [0] * len(sizes)
+    if kind == 'framed':
+        last = [n - d for n, d in zip(sizes, (100, 4 * 4096 + 8, 1))]
     ts = device_streams(sizes, datas=datas)
-    keys, js = ch.tile_records([t.data_ptr() for t in ts], sizes, [0] * len(sizes))
+    keys, js = ch.tile_records([t.data_ptr() for t in ts], sizes, last)
     k0 = int.from_bytes(key[:8], 'little')
     k1 = int.from_bytes(key[8:], 'little')
     base = 0
-    for d, n in zip(datas, sizes):
-        jneed = keys_needed(mx, n, 0)
+    for d, n, P in zip(datas, sizes, last):
+        jneed = keys_needed(mx, n, P)
         nt = jneed // tk + 1 if jneed else 0
         ek = np.zeros(max(nt, 1), np.uint64)
         ej = np.zeros(max(nt, 1), np.uint64)
         buf = np.concatenate([d, np.zeros(16, np.uint8)])
-        o.lib().oc_tile_records(k0, k1, buf.ctypes.data, jneed, tk, nt, ek.ctypes.data,
+        o.lib().oc_tile_records(k0, k1, buf.ctypes.data, n, jneed, tk, nt, ek.ctypes.data,
                                 ej.ctypes.data)
         gk, gj = keys[base:base + nt], js[base:base + nt]
         bad = np.nonzero((gk != ek[:nt]) | ((gj != ej[:nt]) & (ek[:nt] != 0)))[0]
         assert bad.size == 0, (kind, n, bad[:8].tolist(), gk[bad[:4]].tolist(), ek[bad[:4]].tolist(),
                                gj[bad[:4]].tolist(), ej[bad[:4]].tolist())
         base += nt
+
+
+@pytest.mark.parametrize('kind', ['random', 'zeros', 'periodic', 'seeded_key'])
+def test_tile_group_maxima_vs_oracle(kind):
+    """Small-window chunkers: the tile kernel's per-quarter top-16 maxima equal the oracle's
+    for every fast tile; a tile sent to the exact path (the stream ends inside it, or a tie)
+    reports ~0, the no-bound value."""
+    o = _oracle()
+    from replicat_amd.chunker import keys_needed, tile_keys
+    tk = tile_keys()
+    key = synth.seeded_key(11) if kind == 'seeded_key' else b'\xff' * 16
+    mn, mx = 2_000, 80_000
+    ch = GpuChunker(mn, mx, key)
+    sizes = [(3 << 20) + 4 * 321, 1 << 20, 200_004, 1000]
+    rnd = np.random.default_rng(7)
+    if kind == 'zeros':
+        datas = [np.zeros(n, np.uint8) for n in sizes]
+    elif kind == 'periodic':
+        datas = [np.resize(rnd.integers(0, 256, 777, dtype=np.uint8), n) for n in sizes]
+    else:
+        datas = [synth.stream_bytes(n, synth.DEFAULT_SEED, 300 + i) for i, n in enumerate(sizes)]
+    last = [0, (1 << 20) - 100, 0, 0]
+    ts = device_streams(sizes, datas=datas)
+    keys, js, gm = ch.tile_records([t.data_ptr() for t in ts], sizes, last, groups=True)
+    k0 = int.from_bytes(key[:8], 'little')
+    k1 = int.from_bytes(key[8:], 'little')
+    base = exact = 0
+    for d, n, P in zip(datas, sizes, last):
+        jneed = keys_needed(mx, n, P)
+        nt = jneed // tk + 1 if jneed else 0
+        eg = np.zeros(max(nt, 1), np.uint64)
+        buf = np.concatenate([d, np.zeros(16, np.uint8)])
+        o.lib().oc_tile_groups(k0, k1, buf.ctypes.data, n, tk, nt, 4, eg.ctypes.data)
+        g = gm[base:base + nt]
+        ok = (g == eg[:nt]) | (g == np.uint64(2**64 - 1))
+        assert ok.all(), (kind, n, np.nonzero(~ok)[0][:8].tolist())
+        exact += int(((g != eg[:nt]) & (eg[:nt] != np.uint64(2**64 - 1))).sum())
+        base += nt
+    if kind in ('random', 'seeded_key'):
+        assert exact <= 2  # ties inside a lane are rare on random data
 
 
 @pytest.mark.parametrize('walk', ['0', '1'])
