@@ -66,6 +66,10 @@ def main():
             if isinstance(d, dict) and 'FETCH_SIZE' in d:
                 d['hbm_read_bytes_calibrated'] = d['FETCH_SIZE'] * 1024 * factor
     out['workload'] = WORKLOAD
+    # the library build these counters are of (bench.py refuses a summary of another build)
+    sys.path.insert(0, ROOT)
+    from replicat_amd.build import embedded_id
+    out['build_id'] = embedded_id()
     with open(os.path.join(dst, 'pmc_summary.json'), 'w') as f:
         json.dump(out, f, indent=1, sort_keys=True)
     print(json.dumps(out.get('rc_tile_kernel', {}), indent=1))

@@ -138,3 +138,35 @@ def test_encrypted_snapshot(oracle, tmp_path, key_bits, nonce_bits, batch):
     assert len(nonces) == len(res.chunks)
     for f in res.files:
         assert f.digest == hashlib.blake2b(files_data[os.path.basename(f.path)]).digest()
+
+
+@pytest.mark.parametrize('encrypted', [False, True])
+def test_deduplicated_references(oracle, tmp_path, encrypted):
+    """replicat's own dedup cases (test_repository.py:691-736): min = max = 256 over one file
+    of b'A' * 8192 gives 32 chunk references in the file's entry and ONE unique chunk, whose
+    digest is hash_digest of the first chunk -- unencrypted, and encrypted with a random chunker
+    key (a min = max chunker cuts every 256 bytes whatever the key)."""
+    from replicat_amd.pipeline import ChunkEncryption
+    contents = b'A' * 8_192
+    paths = write(tmp_path, {'file': contents})
+    rnd = random.Random(736)
+    enc = ChunkEncryption(shared_key=rnd.randbytes(32), shared_kdf_params=rnd.randbytes(16)) \
+        if encrypted else None
+    params = rnd.randbytes(16) if encrypted else None  # key.params['chunker_params'] (:177)
+    res = DeviceSnapshotProducer(min_length=256, max_length=256, params=params,
+                                 encryption=enc).run(paths)
+    sf = res.snapshot_files()
+    assert len(sf) == 1
+    refs = sf[str(paths[0])]['chunks']
+    assert len(refs) == 32
+    assert len(res.chunks_table) == 1
+    digest = hashlib.blake2b(contents[:256]).digest()
+    assert list(res.chunks_table) == [digest]
+    assert all(c.digest == digest and c.table_index == 0 for c in res.chunks)
+    assert [r['range'] for r in refs] == [[0, 256]] * 32
+    assert res.files[0].digest == hashlib.blake2b(contents).digest()
+    if encrypted:
+        subkey = hashlib.blake2b(digest, salt=enc.shared_kdf_params, key=enc.shared_key,
+                                 digest_size=32).digest()
+        for c in res.chunks:
+            assert oracle.gcm_decrypt(subkey, c.contents[:12], c.contents[12:]) == contents[:256]
