@@ -13,6 +13,7 @@ accumulates pieces into a large host batch and hands the whole batch to the devi
   applies the tail rules of adapters.cpp:48-57 exactly as the reference's final calls do.
 """
 import os
+from abc import ABC, abstractmethod
 from typing import ByteString, Iterator, Optional
 
 import numpy as np
@@ -23,8 +24,26 @@ from .chunker import MAX_LENGTH, MIN_LENGTH, GpuChunker, normalize_params
 # to keep replicat's memory bound (it reads 16 MiB pieces: repository.py:1413,1440)
 DEFAULT_BATCH = 256 << 20
 
+try:  # replicat installed: be one of its chunker adapters (isinstance checks, from_config)
+    from replicat.utils.adapters import ChunkerAdapter
+except ImportError:  # standalone: the same abstract interface, adapters.py:83-103
+    class ChunkerAdapter(ABC):
+        @property
+        @abstractmethod
+        def alignment(self) -> Optional[int]:
+            """Return the alignment"""
 
-class gclmulchunker:
+        @abstractmethod
+        def generate_chunking_params(self) -> bytes:
+            """Generate chunking params"""
+
+        @abstractmethod
+        def __call__(self, chunk_iterator: Iterator[ByteString], *,
+                     params: Optional[bytes] = None) -> Iterator[bytes]:
+            """Re-chunk the incoming stream of bytes using the provided params"""
+
+
+class gclmulchunker(ChunkerAdapter):
     MIN_LENGTH = MIN_LENGTH
     MAX_LENGTH = MAX_LENGTH
     alignment = 4
@@ -36,13 +55,30 @@ class gclmulchunker:
                              f'than the maximum one ({max_length})')
         self.min_length, self.max_length = min_length, max_length
         self.batch_bytes = max(int(batch_bytes), 2 * max_length + 16)
-        self._chunkers = {}
+        self._key = self._gpu = None
 
     def _chunker(self, key16):
-        ch = self._chunkers.get(key16)
-        if ch is None:
-            ch = self._chunkers[key16] = GpuChunker(self.min_length, self.max_length, key16)
-        return ch
+        """The device chunker of the call's key.  One is kept (a repository uses one key), so a
+        long-lived adapter does not pile up device tables and staging buffers per key; the
+        reference builds a fresh native chunker per __call__ (adapters.py:287-289)."""
+        if self._key != key16:
+            # the previous chunker is dropped, not closed: a generator of an earlier call may
+            # still hold it (GpuChunker.__del__ releases it with its last reference)
+            self._gpu = GpuChunker(self.min_length, self.max_length, key16)
+            self._key = key16
+        return self._gpu
+
+    def close(self):
+        """Release the device chunker (tables, workspaces, pinned staging)."""
+        gpu, self._gpu, self._key = self._gpu, None, None
+        if gpu is not None:
+            gpu.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
     def __call__(self, chunk_iterator: Iterator[ByteString], *,
                  params: Optional[bytes] = None) -> Iterator[bytes]:

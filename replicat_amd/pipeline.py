@@ -54,6 +54,7 @@ class FileRecord:
     stream_start: int
     stream_end: int
     digest: Optional[bytes] = None
+    size: Optional[int] = None   # at open time (fstat of the opened file), when it tells
 
 
 @dataclass
@@ -123,6 +124,10 @@ def tagged_pieces(paths: Sequence[str], files: List[FileRecord], read=None
         files.append(f)
         prev = f
         with (read(path) if read else open(path, 'rb')) as src:
+            try:
+                f.size = os.fstat(src.fileno()).st_size
+            except (AttributeError, OSError, ValueError):
+                f.size = None  # a read hook without a file descriptor
             while piece := src.read(PIECE):
                 pos += len(piece)
                 f.stream_end += len(piece)
@@ -192,21 +197,20 @@ class DeviceSnapshotProducer:
     # work; 'device' and 'host' force one engine.
     HOST_DIGEST_MIN = 1 << 20
 
-    def _on_host(self, fi, f, read, hstates):
-        if fi in hstates:
-            return True
-        if self.file_digests == 'device':
-            return False
-        if self.file_digests == 'auto':
-            try:
-                size = os.stat(f.path).st_size if read is None else 0
-            except OSError:
-                size = 0
-            if size < self.HOST_DIGEST_MIN:
-                return False
-        import hashlib
-        hstates[fi] = hashlib.blake2b(digest_size=self.digest_size)
-        return True
+    def _on_host(self, fi, f, hstates, engine):
+        """Whether file fi's digest runs on a host thread; decided once per file (its bytes must
+        all go to one engine): in 'auto' by the size fstat gave when the file was opened, or,
+        for a read hook with no file descriptor, by the bytes read when it is first seen."""
+        if fi not in engine:
+            if self.file_digests == 'auto':
+                size = f.size if f.size is not None else f.stream_end - f.stream_start
+                engine[fi] = size >= self.HOST_DIGEST_MIN
+            else:
+                engine[fi] = self.file_digests == 'host'
+            if engine[fi]:
+                import hashlib
+                hstates[fi] = hashlib.blake2b(digest_size=self.digest_size)
+        return engine[fi]
 
     def _host_pool(self):
         if self._pool is None:
@@ -226,6 +230,7 @@ class DeviceSnapshotProducer:
         table: Dict[bytes, int] = {}
         states = {}              # file index -> device state (open files only)
         hstates = {}             # file index -> host hasher (open large files only)
+        engine = {}              # file index -> its digest runs on the host (decided once)
         finalized = 0            # files [0, finalized) have their digest
         hnp = self.host.numpy()
         buf_start = 0            # stream offset of host[0]
@@ -255,7 +260,7 @@ class DeviceSnapshotProducer:
             lo_stream, hi_stream = buf_start + fed, buf_start + blen
             host_jobs = []       # (file index, future or None, final)
             for fi in range(finalized, len(files)):
-                if not self._on_host(fi, files[fi], read, hstates):
+                if not self._on_host(fi, files[fi], hstates, engine):
                     continue
                 f = files[fi]
                 a, b = max(f.stream_start, lo_stream), min(f.stream_end, hi_stream)
@@ -290,7 +295,7 @@ class DeviceSnapshotProducer:
             # ---- device: per-file incremental digests over the fresh bytes [fed, blen)
             items = []           # (file index, device ptr, length, final)
             for fi in range(finalized, len(files)):
-                if fi in hstates:
+                if engine.get(fi):
                     continue
                 f = files[fi]
                 a, b = max(f.stream_start, lo_stream), min(f.stream_end, hi_stream)

@@ -170,3 +170,18 @@ def test_deduplicated_references(oracle, tmp_path, encrypted):
                                  digest_size=32).digest()
         for c in res.chunks:
             assert oracle.gcm_decrypt(subkey, c.contents[:12], c.contents[12:]) == contents[:256]
+
+
+def test_read_hook_without_fileno(tmp_path):
+    """A read hook whose objects have no file descriptor: each file's digest engine is decided
+    once, from the bytes read when the file is first seen, and every digest still equals
+    hashlib's across batches (large files straddle them)."""
+    import io
+    rnd = random.Random(42)
+    files_data = {'f%02d' % i: rnd.randbytes(n) for i, n in
+                  enumerate([0, 100, 5000, (1 << 20) + 3, (3 << 20) + 1, 700_000])}
+    paths = write(tmp_path, files_data)
+    prod = DeviceSnapshotProducer(min_length=2_000, max_length=80_000, batch_bytes=1 << 20)
+    res = prod.run(paths, read=lambda p: io.BytesIO(files_data[os.path.basename(str(p))]))
+    check_stream(res, files_data)
+    assert all(f.size is None for f in res.files)
