@@ -159,6 +159,7 @@ int rc_fail(int code, const char *fmt, ...) {
 
 struct rc_chunker {
     uint64_t min_length = 0, max_length = 0, window = 0;
+    bool small = false;   // window + 2 edge tiles within 64 tiles (the chain's one-row cache)
     bool groups = false;  // small windows: the tile kernel also writes per-group maxima
     uint64_t seg_force = 0, ext_steps = 2;  // segment-parallel chains (see stage_descriptors)
     uint64_t k0 = 0, k1 = 0;
@@ -201,7 +202,7 @@ struct rc_chunker {
 namespace {
 
 struct Plan {
-    uint64_t n = 0, n_tiles = 0, total_cap = 0;
+    uint64_t n = 0, n_tiles = 0, total_cap = 0, max_len = 0;
     uint64_t n_segs = 0, scratch_entries = 0;
     uint64_t seg_bytes = 0, seg_cap = 0;
     bool any_multi = false;
@@ -319,6 +320,7 @@ int stage_descriptors(rc_chunker *ch, Workspace &ws, uint64_t n, const uint8_t *
             plan.any_multi = true;
         }
         const uint64_t jneed = rc_keys_needed(ch->max_length, L, P);
+        plan.max_len = std::max(plan.max_len, L);
         u[i] = reinterpret_cast<uint64_t>(ptrs[i]);
         u[n + i] = L;
         u[2 * n + i] = P;
@@ -376,6 +378,8 @@ int upload_and_launch(rc_chunker *ch, Workspace &ws, const Plan &plan, ChainPara
     }
     uint64_t *gmax = ch->groups ? group_maxima(ws, plan) : nullptr;
     prm.gmax = gmax;
+    // 32-bit chain steps: small windows (the one-row record cache) and key indices < 2^32
+    prm.lean = ch->small && plan.max_len < (16ull << 30) ? 1u : 0u;
     if (rc_launch_tiles(ch->d_tables, d, plan.n, plan.n_tiles,
                         static_cast<TileRecord *>(ws.d_records.p), gmax, stream,
                         ch->timing ? ev[1] : nullptr))
@@ -407,6 +411,7 @@ ChainParams chain_params(const rc_chunker *ch, const Plan &plan, uint64_t max_st
     p.seg_cap = plan.seg_cap;
     p.ext_steps = ch->ext_steps;
     p.gmax = nullptr;  // set per launch (upload_and_launch)
+    p.lean = 0;
     return p;
 }
 
@@ -473,8 +478,10 @@ int rc_chunker_create(uint64_t min_length, uint64_t max_length, const uint8_t *k
     ch->window = window_keys(max_length);
     // a window (plus its two edge tiles) within one 64-tile row of the chain's record cache:
     // the chain's edge ranges are then a large part of its work, and group maxima trim them
-    ch->groups = ch->window / kTileKeys + 3 <= 64;
+    ch->small = ch->window / kTileKeys + 3 <= 64;
+    ch->groups = ch->small;
     if (const char *e = getenv("RC_TILE_GROUPS_OFF")) ch->groups = ch->groups && e[0] != '1';
+    if (const char *e = getenv("RC_CHAIN_LEAN_OFF")) ch->small = ch->small && e[0] != '1';
     ch->k0 = k0;
     ch->k1 = k1;
     ch->device = device;

@@ -75,6 +75,7 @@ struct ChainParams {
     uint64_t ext_steps;   // steps a speculative chain runs past its segment end
     const uint64_t *gmax; // per-tile group maxima (rc_launch_tiles), or NULL
     uint32_t open;        // RC_OPEN: non-final prefix, no tail rule
+    uint32_t lean;        // small windows and every stream < 16 GiB: 32-bit chain steps
 };
 
 // splitmix64 finaliser (replicat_amd/synth.py)

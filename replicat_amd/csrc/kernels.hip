@@ -834,15 +834,15 @@ __device__ __forceinline__ bool trim_groups(uint64_t gm, uint64_t te, uint32_t t
 // tiles outside it reloads the span from its first needed tile (one round trip, as before).
 template <int R>
 struct RecCache {
-    uint64_t c0 = 0, n = 0;  // cached stream tiles [c0, c0 + n)
+    uint32_t c0 = 0, n = 0;  // cached stream tiles [c0, c0 + n) (a stream has < 2^32 tiles)
     TileRecord v[R];
     uint64_t g[R];           // group maxima of the same tiles (when the tile kernel made them)
 
     __device__ bool has(uint64_t t) const { return t >= c0 && t - c0 < n; }
     __device__ void load(const TileRecord *rec, const uint64_t *gmax, const ChainStream &st,
                          uint64_t lo) {
-        c0 = lo;
-        n = min(st.nt - lo, (uint64_t)64 * R);
+        c0 = (uint32_t)lo;
+        n = (uint32_t)min(st.nt - lo, (uint64_t)64 * R);
         const uint64_t lane = lane_id();
 #pragma unroll
         for (int u = 0; u < R; ++u)
@@ -1070,6 +1070,217 @@ __device__ int chain_step(const uint64_t *tl, const uint64_t *th, const uint32_t
     return kStepTail1;
 }
 
+// ---- the chain step for small windows (prm.lean): the same decisions as chain_step, with the
+// window's tiles in the one cached record row and key indices in 32 bits (streams below
+// 16 GiB).  chain_step's 64-bit uniform compares are VALU instructions on gfx950 (there is no
+// 64-bit SALU compare) and its live ranges spill SGPRs to VGPR lanes; at ~25 steps per 1 MiB
+// stream that overhead, not memory, set the chain's time (rocprofv3 SQ counters,
+// profiles/r02/chain_pmc_3iii_groups.txt).
+
+__device__ __forceinline__ bool ge64(uint64_t a, uint32_t b) {  // a >= b with SALU compares
+    return (uint32_t)(a >> 32) != 0u || (uint32_t)a >= b;
+}
+
+__device__ __forceinline__ void take_best32(uint64_t k, uint32_t j, uint64_t &bk, uint32_t &bj) {
+    if (k > bk || (k == bk && j < bj)) {
+        bk = k;
+        bj = j;
+    }
+}
+
+// trim_groups on 32-bit indices: the range [a, b] inside tile te, emptied as a > b
+__device__ __forceinline__ void trim_groups32(uint64_t gm, uint32_t te, uint32_t tb16,
+                                              uint32_t &a, uint32_t &b) {
+    const uint32_t tj0 = te * kTileKeys;
+    uint32_t ga = (a - tj0) / kGroupKeys, gb = (b - tj0) / kGroupKeys;
+    while (ga <= gb && ((gm >> (16 * ga)) & 0xffffu) < tb16) ++ga;
+    while (gb > ga && ((gm >> (16 * gb)) & 0xffffu) < tb16) --gb;
+    if (ga > gb) {
+        a = 1;
+        b = 0;
+        return;
+    }
+    a = max(a, tj0 + ga * kGroupKeys);
+    b = min(b, tj0 + (gb + 1) * kGroupKeys - 1);
+}
+
+__device__ int chain_step_small(const uint64_t *tl, const uint64_t *th, const uint32_t *pf,
+                                const TileRecord *rec, const ChainStream &st,
+                                const ChainParams &prm, RecCache<1> &cache, uint64_t pos,
+                                uint32_t lb_a, uint32_t lb_b, uint64_t &c1, uint64_t &c2) {
+    const uint32_t minl = (uint32_t)prm.min_length, maxl = (uint32_t)prm.max_length;
+    const uint32_t T = (uint32_t)prm.window;
+    const bool single = prm.max_steps == 0;
+    const uint64_t rem = st.L - pos;
+    const bool argmax = single || (st.P >= pos && ge64(st.P - pos, maxl)) || ge64(rem, 2 * maxl);
+    if (prm.open && !argmax) return kStepStop;
+    if (argmax) {
+        const uint32_t s4 = (uint32_t)(pos >> 2), jmax = (uint32_t)st.jmax;
+        const uint32_t ja = s4 + 1, jb = min(s4 + T, jmax);
+        uint64_t bk = 0;
+        uint32_t bj = ~0u;
+        if (T > 0 && ja <= jb) {
+            const uint32_t t_lo = (ja + kTileKeys - 1) / kTileKeys, t_hi = (jb + 1) / kTileKeys;
+            const bool have_rec = t_lo < t_hi;
+            uint32_t a0 = ja, b0 = jb, a1 = 1, b1 = 0;
+            if (have_rec) {
+                b0 = t_lo * kTileKeys - 1;
+                a1 = t_hi * kTileKeys;
+                b1 = jb;
+            }
+            const bool one0 = a0 <= b0 && a0 / kTileKeys == b0 / kTileKeys;
+            const bool one1 = a1 <= b1 && a1 / kTileKeys == b1 / kTileKeys;
+            const uint32_t te0 = a0 / kTileKeys, te1 = a1 / kTileKeys;
+            uint32_t need_lo = have_rec ? t_lo : ~0u, need_hi = have_rec ? t_hi - 1 : 0u;
+            if (one0) {
+                need_lo = min(need_lo, te0);
+                need_hi = max(need_hi, te0);
+            }
+            if (one1) {
+                need_lo = min(need_lo, te1);
+                need_hi = max(need_hi, te1);
+            }
+            if (need_lo <= need_hi && !(cache.has(need_lo) && cache.has(need_hi)))
+                cache.load(rec, prm.gmax, st, need_lo);  // covers them all: window + 2 <= 64 tiles
+            const uint32_t lane = lane_id();
+            const uint64_t key = cache.v[0].key;
+            // the full tiles' best record: the lanes' key high words, then (on a tie) the low
+            // words, then the lowest lane -- the lowest tile, hence the lowest index
+            if (have_rec) {
+                const uint32_t t = cache.c0 + lane;
+                const bool inr = lane < cache.n && t >= t_lo && t < t_hi && key != 0;
+                const uint32_t hi = inr ? (uint32_t)(key >> 32) : 0u;
+                const uint32_t mhi = wave_max_u32(hi);
+                const bool top = inr && hi == mhi;
+                uint64_t m = __ballot(top);
+                if (m & (m - 1)) {
+                    const uint32_t lo = top ? (uint32_t)key : 0u;
+                    const uint32_t mlo = wave_max_u32(lo);
+                    m = __ballot(top && lo == mlo);
+                }
+                if (m) {
+                    const int w = __builtin_ctzll(m);
+                    bk = lane_u64(key, w);
+                    bj = (uint32_t)__builtin_amdgcn_readlane((uint32_t)cache.v[0].j, w);
+                }
+            }
+            uint64_t ek0 = 0, ek1 = 0, gm0 = ~0ull, gm1 = ~0ull;
+            uint32_t ej0 = 0, ej1 = 0;
+            if (one0) {
+                const int l = (int)(te0 - cache.c0);
+                ek0 = lane_u64(key, l);
+                ej0 = (uint32_t)__builtin_amdgcn_readlane((uint32_t)cache.v[0].j, l);
+                if (prm.gmax) gm0 = lane_u64(cache.g[0], l);
+            }
+            if (one1) {
+                const int l = (int)(te1 - cache.c0);
+                ek1 = lane_u64(key, l);
+                ej1 = (uint32_t)__builtin_amdgcn_readlane((uint32_t)cache.v[0].j, l);
+                if (prm.gmax) gm1 = lane_u64(cache.g[0], l);
+            }
+            // settle the edge ranges by their tiles' records, then trim them by the group
+            // maxima (chain_step explains both rules)
+            bool live0 = a0 <= b0, live1 = a1 <= b1;
+            if (one0 && (ek0 == 0 || (ej0 >= a0 && ej0 <= b0) || ek0 < bk)) {
+                if (ek0 != 0 && ej0 >= a0 && ej0 <= b0) take_best32(ek0, ej0, bk, bj);
+                live0 = false;
+            }
+            if (one1 && (ek1 == 0 || (ej1 >= a1 && ej1 <= b1) || ek1 <= bk)) {
+                if (ek1 != 0 && ej1 >= a1 && ej1 <= b1) take_best32(ek1, ej1, bk, bj);
+                live1 = false;
+            }
+            if (prm.gmax) {
+                const uint32_t tb16 = (uint32_t)(bk >> 48);
+                if (one0 && live0) {
+                    trim_groups32(gm0, te0, tb16, a0, b0);
+                    live0 = a0 <= b0;
+                }
+                if (one1 && live1) {
+                    trim_groups32(gm1, te1, tb16, a1, b1);
+                    live1 = a1 <= b1;
+                }
+            }
+            if (live0 || live1) {
+                if (!live0) {
+                    a0 = 1;
+                    b0 = 0;
+                }
+                if (!live1) {
+                    a1 = 1;
+                    b1 = 0;
+                }
+                EdgeRange r0, r1;
+                r0.init(st.base, st.L / 4 - 1, a0, b0, 0);
+                r1.init(st.base, st.L / 4 - 1, a1, b1, 1);
+                uint32_t w0[kEdgeIters][4], w1[kEdgeIters][4];
+                uint32_t acc_first = 0, acc_last = 0;
+                if (r0.more()) r0.load(w0);
+                if (r1.more()) r1.load(w1);
+                for (;;) {
+                    const bool m0 = r0.more(), m1 = r1.more();
+                    if (!m0 && !m1) break;
+                    if (m0) {
+                        r0.template compute<true>(w0, lb_a, lb_b, pf, acc_first, acc_last);
+                        if (r0.more()) r0.load(w0);
+                    }
+                    if (m1) {
+                        r1.template compute<true>(w1, lb_a, lb_b, pf, acc_first, acc_last);
+                        if (r1.more()) r1.load(w1);
+                    }
+                }
+                const uint32_t m = wave_max_u32(acc_first);
+                if ((m & 0x8000u) && (m >> 16) >= (uint32_t)(bk >> 48)) {
+                    const bool cand = (acc_first >> 16) == (m >> 16) && (acc_first & 0x8000u);
+                    const uint32_t fl = 511u - (acc_first & 0x1ffu), ll = acc_last & 0x1ffu;
+                    if (__any(cand && fl != ll)) {
+                        // a candidate lane holds its top-16 maximum twice: exact scan
+                        uint64_t ek = 0, ej = ~0ull;
+                        scan_ranges<kChainScanUnroll>(tl, th, st.base, a0, b0, a1, b1, ek, ej);
+                        uint64_t bj64 = bj == ~0u ? ~0ull : bj;
+                        take_best(ek, ej, bk, bj64);
+                        wave_best(bk, bj64);
+                        bj = (uint32_t)bj64;
+                    } else {
+                        const uint32_t lo = fl & 255u;  // lane-local index within its range
+                        const uint32_t jc = ((fl < 256 ? a0 : a1) & ~3u) + 256u * (lo >> 2) +
+                                            4u * lane + (lo & 3);
+                        const uint32_t jl = cand ? jc : a0 <= b0 ? a0 : a1;  // any valid index
+                        const uint64_t k = full_key(tl, th, ld_u32(st.base + 4ull * jl - 4),
+                                                    ld_u32(st.base + 4ull * jl));
+                        for (uint64_t cm = __ballot(cand); cm; cm &= cm - 1) {
+                            const int l = __builtin_ctzll(cm);
+                            take_best32(lane_u64(k, l),
+                                        (uint32_t)__builtin_amdgcn_readlane(jl, l), bk, bj);
+                        }
+                    }
+                }
+            }
+        }
+        uint32_t idx = bk > 0 ? 4u * (bj - s4) : 0u;
+        if (idx < minl) idx = (minl + 3) & ~3u;  // adapters.cpp:66-67
+        if (single) {
+            c1 = idx;
+            return kStepCut;
+        }
+        if (idx != 0) {
+            c1 = pos + idx;
+            return kStepCut;
+        }
+        if (ge64(rem, 2 * maxl) || prm.open) return kStepStop;  // min_length == 0 (S7 UB)
+    }
+    uint64_t c;
+    if (rem <= maxl) c = rem;
+    else if (rem < (uint64_t)maxl + minl) c = rem / 2;
+    else c = maxl;
+    if (c == 0) return kStepStop;
+    c1 = pos + c;
+    if (c < rem) {
+        c2 = st.L;
+        return kStepTail2;
+    }
+    return kStepTail1;
+}
+
 __device__ __forceinline__ uint64_t find_index(const uint64_t *base_arr, uint64_t n, uint64_t v) {
     uint64_t lo = 0, hi = n;  // largest i with base_arr[i] <= v
     while (hi - lo > 1) {
@@ -1086,7 +1297,7 @@ __device__ __forceinline__ uint64_t find_index(const uint64_t *base_arr, uint64_
 // Workgroups of kChainWaves walkers on 20 KiB of LDS.  R = rows of the record cache: 1 for
 // windows of up to ~60 tiles (max_length below ~1 MB: a 1 MiB stream's records load once),
 // 4 otherwise (a default window spans 313 tiles and reloads every step, as it must).
-template <int R>
+template <int R, bool kLean>
 __global__ __launch_bounds__(kChainWaves * 64) void rc_spec_kernel(const KeyTables *__restrict__ tab,
                                                       StreamDesc d, uint64_t n_streams,
                                                       ChainParams prm, uint64_t n_segs,
@@ -1132,7 +1343,13 @@ __global__ __launch_bounds__(kChainWaves * 64) void rc_spec_kernel(const KeyTabl
         }
         if (!direct && pos >= seg_end && ext++ >= prm.ext_steps) break;
         uint64_t c1 = 0, c2 = 0;
-        const int kind = chain_step<R>(tl, th, pf, rec, st, prm, cache, pos, lb_a, lb_b, c1, c2);
+        int kind;
+        if constexpr (kLean) {
+            static_assert(R == 1, "the lean step works on the one-row cache");
+            kind = chain_step_small(tl, th, pf, rec, st, prm, cache, pos, lb_a, lb_b, c1, c2);
+        } else {
+            kind = chain_step<R>(tl, th, pf, rec, st, prm, cache, pos, lb_a, lb_b, c1, c2);
+        }
         if (kind == kStepStop) {
             term = true;
             break;
@@ -1577,12 +1794,16 @@ int rc_launch_chain(const KeyTables *d_tables, StreamDesc desc, uint64_t n_strea
     // 4-wave workgroups on 20 KiB of LDS (compact tables)
     const bool small = prm.window / kTileKeys + 3 <= 64;  // window + both edge tiles in one row
     const uint64_t grid = (n_segs + kChainWaves - 1) / kChainWaves;
-    if (small)
-        hipLaunchKernelGGL(rc_spec_kernel<1>, dim3((unsigned)grid), dim3(kChainWaves * kWaveSize),
-                           0, st, d_tables, desc, n_streams, prm, n_segs, d_records, d_cuts,
-                           d_counts, d_scratch, d_seg_counts);
+    if (small && prm.lean)
+        hipLaunchKernelGGL((rc_spec_kernel<1, true>), dim3((unsigned)grid),
+                           dim3(kChainWaves * kWaveSize), 0, st, d_tables, desc, n_streams, prm,
+                           n_segs, d_records, d_cuts, d_counts, d_scratch, d_seg_counts);
+    else if (small)
+        hipLaunchKernelGGL((rc_spec_kernel<1, false>), dim3((unsigned)grid),
+                           dim3(kChainWaves * kWaveSize), 0, st, d_tables, desc, n_streams, prm,
+                           n_segs, d_records, d_cuts, d_counts, d_scratch, d_seg_counts);
     else
-        hipLaunchKernelGGL(rc_spec_kernel<kRecUnroll>, dim3((unsigned)grid),
+        hipLaunchKernelGGL((rc_spec_kernel<kRecUnroll, false>), dim3((unsigned)grid),
                            dim3(kChainWaves * kWaveSize), 0, st, d_tables, desc, n_streams, prm,
                            n_segs, d_records, d_cuts, d_counts, d_scratch, d_seg_counts);
     if (launch_status("rc_spec_kernel")) return 1;

@@ -47,6 +47,7 @@ def _window_runner(ch, windows_bufs):
         buf = windows_bufs[w.start]
         st = bench.Config3ii.__new__(bench.Config3ii)
         st.ch, st.hs, st.buf = ch, fake.hs, buf
+        st.be = bench.Backend(torch.cuda.current_device())
         _, caps = ch.capacity([w.end - w.start])
         st.cap = int(caps[0])
         st.cuts = torch.zeros(st.cap + 1, dtype=torch.int64, device='cuda')
