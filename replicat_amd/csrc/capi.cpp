@@ -161,7 +161,7 @@ struct rc_chunker {
     uint64_t min_length = 0, max_length = 0, window = 0;
     bool small = false;   // window + 2 edge tiles within 64 tiles (the chain's one-row cache)
     bool groups = false;  // small windows: the tile kernel also writes per-group maxima
-    uint64_t seg_force = 0, ext_steps = 2;  // segment-parallel chains (see stage_descriptors)
+    uint64_t seg_force = 0, ext_steps = 4;  // segment-parallel chains (see stage_descriptors)
     uint64_t k0 = 0, k1 = 0;
     int device = 0;
     KeyTables tables;
@@ -175,6 +175,7 @@ struct rc_chunker {
         DevBuf d_records;   // one TileRecord per tile
         DevBuf d_scratch;   // speculative chain lists of multi-segment streams
         DevBuf d_seg_counts;  // one count (+ termination bit) per chain segment
+        std::vector<uint64_t> xtiles;  // host list of the tiles the fast path does not take
         hipEvent_t done = nullptr;  // the call that last used this workspace has finished
         bool pending = false;
     } ws[2];
@@ -210,7 +211,8 @@ struct Plan {
 };
 
 // Layout of the descriptor buffer: ptr[n] len[n] last[n] jneed[n] tile_base[n+1] cut_base[n]
-// cut_cap[n] seg_base[n+1] scratch_base[n], all u64.
+// cut_cap[n] seg_base[n+1] scratch_base[n] xtiles[1 + k], all u64 (xtiles: the count k, then
+// the global indices of the tiles the fast path does not take).
 StreamDesc desc_view(void *base, uint64_t n) {
     uint64_t *u = static_cast<uint64_t *>(base);
     StreamDesc d;
@@ -223,6 +225,7 @@ StreamDesc desc_view(void *base, uint64_t n) {
     d.cut_cap = u + 6 * n + 1;
     d.seg_base = u + 7 * n + 1;
     d.scratch_base = u + 8 * n + 2;
+    d.xtiles = u + 9 * n + 2;
     return d;
 }
 
@@ -277,13 +280,32 @@ int stage_descriptors(rc_chunker *ch, Workspace &ws, uint64_t n, const uint8_t *
                       const uint64_t *lens, const uint64_t *last, Plan &plan, bool open = false,
                       bool single = false) {
     plan.n = n;
-    plan.bytes = (9 * n + 2) * sizeof(uint64_t);
     if (ws.pending) {  // the call that used this workspace before must be done with it
         HIP_TRY(hipEventSynchronize(ws.done));
         ws.pending = false;
     }
+    // tiles the fast path does not take (kernels.hip tile_fast): a stream's tile 0 when the
+    // stream is shorter than a tile, and its last tile when the stream ends inside it
+    std::vector<uint64_t> &xt = ws.xtiles;
+    xt.clear();
+    {
+        uint64_t tiles = 0;
+        for (uint64_t i = 0; i < n; ++i) {
+            const uint64_t L = lens[i], P = open ? L : (last ? last[i] : 0);
+            const uint64_t jneed = rc_keys_needed(ch->max_length, L, P);
+            const uint64_t nt = jneed ? jneed / kTileKeys + 1 : 0;
+            const uint64_t jmax = L >= 8 ? (L - 4) / 4 : 0;
+            auto fast = [&](uint64_t t) { return L >= 8 && t * kTileKeys + kTileKeys - 1 <= jmax; };
+            if (nt && !fast(0)) xt.push_back(tiles);
+            if (nt > 1 && !fast(nt - 1)) xt.push_back(tiles + nt - 1);  // the tiles between are fast
+            tiles += nt;
+        }
+    }
+    plan.bytes = (9 * n + 3 + xt.size()) * sizeof(uint64_t);
     if (int rc = ws.h_desc.ensure(plan.bytes)) return rc;
     uint64_t *u = static_cast<uint64_t *>(ws.h_desc.p);
+    u[9 * n + 2] = xt.size();
+    std::copy(xt.begin(), xt.end(), u + 9 * n + 3);
     // Chain segments.  The chain of a stream is one wave walking ~(bound / chunk) steps; split
     // a stream only when the batch has too few streams to keep ~kChainWalkers waves busy, and
     // never below 3 * max_length per segment (speculative chains must meet inside it).
@@ -346,11 +368,20 @@ uint64_t *group_maxima(Workspace &ws, const Plan &plan) {
                                         (plan.n_tiles + 1) * sizeof(TileRecord));
 }
 
+// the tile kernel's per-wave tie lists: n_tiles slots + one count per wave (<= n_tiles + 16)
+uint32_t *tie_lists(Workspace &ws, const Plan &plan) {
+    return reinterpret_cast<uint32_t *>(group_maxima(ws, plan) + plan.n_tiles + 1);
+}
+
+size_t records_bytes(const Plan &plan) {
+    return (plan.n_tiles + 1) * (sizeof(TileRecord) + 8) + (2 * plan.n_tiles + 32) * 4;
+}
+
 int upload_and_launch(rc_chunker *ch, Workspace &ws, const Plan &plan, ChainParams prm,
                       uint64_t *d_cuts, int64_t *d_counts, hipStream_t stream) {
     if (int rc = ws.d_desc.ensure(plan.bytes)) return rc;
-    // records, then (small windows) the group maxima of every tile
-    if (int rc = ws.d_records.ensure((plan.n_tiles + 1) * (sizeof(TileRecord) + 8))) return rc;
+    // records, then (small windows) the group maxima of every tile, then the tie lists
+    if (int rc = ws.d_records.ensure(records_bytes(plan))) return rc;
     if (int rc = ws.d_scratch.ensure(std::max<uint64_t>(plan.scratch_entries, 1) * 8)) return rc;
     // counts, merge points, slice offsets and slices of the parallel join (kernels.hip)
     if (int rc = ws.d_seg_counts.ensure(std::max<uint64_t>(plan.n_segs, 1) * 32)) return rc;
@@ -381,8 +412,8 @@ int upload_and_launch(rc_chunker *ch, Workspace &ws, const Plan &plan, ChainPara
     // 32-bit chain steps: small windows (the one-row record cache) and key indices < 2^32
     prm.lean = ch->small && plan.max_len < (16ull << 30) ? 1u : 0u;
     if (rc_launch_tiles(ch->d_tables, d, plan.n, plan.n_tiles,
-                        static_cast<TileRecord *>(ws.d_records.p), gmax, stream,
-                        ch->timing ? ev[1] : nullptr))
+                        static_cast<TileRecord *>(ws.d_records.p), gmax, tie_lists(ws, plan),
+                        stream, ch->timing ? ev[1] : nullptr))
         return fail(RC_ERR_HIP, "%s", rc_launch_error());
     if (ch->timing) HIP_TRY(hipEventRecord(ev[2], stream));
     if (rc_launch_chain(ch->d_tables, d, plan.n, prm, plan.n_segs,
@@ -490,7 +521,10 @@ int rc_chunker_create(uint64_t min_length, uint64_t max_length, const uint8_t *k
         // chain segmentation knobs (RC_SEGMENT_BYTES forces a segment length; RC_SEGMENT_EXT
         // sets the speculative extension); the per-call choice is made in stage_descriptors
         if (const char *e = getenv("RC_SEGMENT_BYTES")) ch->seg_force = strtoull(e, nullptr, 0);
-        ch->ext_steps = 2;
+        // 4 steps past the segment end: with 2, one of the harness stream's 332 segment
+        // boundaries (segments of 3 x max) failed to meet the next chain, and one failure sends
+        // the whole stream to the sequential join (0.58 ms instead of 0.13)
+        ch->ext_steps = 4;
         if (const char *e = getenv("RC_SEGMENT_EXT")) ch->ext_steps = strtoull(e, nullptr, 0);
     }
     {
@@ -776,11 +810,12 @@ int rc_tile_records(rc_chunker *ch, uint64_t n, const uint8_t *const *d_streams,
     Workspace &ws = acquire_ws(ch);
     if (int rc = stage_descriptors(ch, ws, n, d_streams, lens, last_piece, plan)) return rc;
     if (int rc = ws.d_desc.ensure(plan.bytes)) return rc;
-    if (int rc = ws.d_records.ensure((plan.n_tiles + 1) * (sizeof(TileRecord) + 8))) return rc;
+    if (int rc = ws.d_records.ensure(records_bytes(plan))) return rc;
     HIP_TRY(hipMemcpy(ws.d_desc.p, ws.h_desc.p, plan.bytes, hipMemcpyHostToDevice));
     uint64_t *d_gmax = ch->groups ? group_maxima(ws, plan) : nullptr;
     if (rc_launch_tiles(ch->d_tables, desc_view(ws.d_desc.p, n), n, plan.n_tiles,
-                        static_cast<TileRecord *>(ws.d_records.p), d_gmax, nullptr, nullptr))
+                        static_cast<TileRecord *>(ws.d_records.p), d_gmax, tie_lists(ws, plan),
+                        nullptr, nullptr))
         return fail(RC_ERR_HIP, "%s", rc_launch_error());
     HIP_TRY(hipDeviceSynchronize());
     std::vector<TileRecord> h(plan.n_tiles);

@@ -56,6 +56,7 @@ struct StreamDesc {
     const uint64_t *cut_cap;    // n entries
     const uint64_t *seg_base;   // n+1 entries, exclusive prefix sum of chain segments per stream
     const uint64_t *scratch_base;  // n entries: offset of the stream's speculative lists
+    const uint64_t *xtiles;        // count, then the tiles that are not fast (tile_fast), global
 };
 
 // One record per tile: first maximal key of the tile and its key index in the stream.
@@ -94,9 +95,11 @@ extern "C" {
 // d_gmax (may be NULL): n_tiles + 1 words of per-group top-16 maxima (kTileGroups x u16 per
 // tile) -- the chain's bounds for small windows.  mid_event (a hipEvent_t, may be NULL):
 // recorded between the tile and the edge kernel.
+// d_xlist: n_tiles + (one count per tile-kernel wave: at most n_tiles) u32 of scratch for the
+// tile kernel's per-wave tie lists.
 int rc_launch_tiles(const rc::KeyTables *d_tables, rc::StreamDesc desc, uint64_t n_streams,
-                    uint64_t n_tiles, rc::TileRecord *d_records, uint64_t *d_gmax, void *stream,
-                    void *mid_event);
+                    uint64_t n_tiles, rc::TileRecord *d_records, uint64_t *d_gmax,
+                    uint32_t *d_xlist, void *stream, void *mid_event);
 int rc_launch_chain(const rc::KeyTables *d_tables, rc::StreamDesc desc, uint64_t n_streams,
                     rc::ChainParams prm, uint64_t n_segs, const rc::TileRecord *d_records,
                     uint64_t *d_cuts, int64_t *d_counts, uint64_t *d_scratch,

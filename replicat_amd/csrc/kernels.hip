@@ -463,12 +463,19 @@ __device__ __forceinline__ void stage_tile_tables(const KeyTables *tab) {
 // G > 1: also gmax[t] = the top-16 maximum of each of the tile's G key groups (u16 g at bits
 // 16g; keys that do not exist count as 0), an upper bound the chain uses to leave most of an
 // edge range unscanned (chain_step).
+//
+// Tiles the fast path cannot settle -- a candidate lane holding its top-16 maximum twice --
+// are listed per wave for the edge kernel: xlist[t_begin + i] (i < xcount[wave]).  Every tile
+// stores its index at the list's next slot and only a tie advances the count, so the store is
+// unconditional and every tile keeps the same vector-memory sequence.
 template <int G>
 __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restrict__ tab,
                                                        StreamDesc d, uint64_t n_streams,
                                                        uint64_t n_tiles,
                                                        TileRecord *__restrict__ rec,
-                                                       uint64_t *__restrict__ gmax) {
+                                                       uint64_t *__restrict__ gmax,
+                                                       uint32_t *__restrict__ xlist,
+                                                       uint32_t *__restrict__ xcount) {
     stage_tile_tables(tab);
     const uint64_t *full = reinterpret_cast<const uint64_t *>(s_tile_lds + kFullOff / 4);
     const uint64_t *tl = full, *th = full + 1024;
@@ -479,14 +486,21 @@ __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restri
     const uint64_t gw = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
     const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
     uint64_t t = n_tiles * gw / nw;
-    const uint64_t t_end = n_tiles * (gw + 1) / nw;
-    if (t >= t_end) return;
+    const uint64_t t_begin = t, t_end = n_tiles * (gw + 1) / nw;
+    uint32_t n_ties = 0;
+    if (t >= t_end) {
+        if (lane == 0) xcount[gw] = 0;
+        return;
+    }
 
     TileCursor cursor;
     cursor.init(d, n_streams, t);
     TileRef cur = cursor.at(t);
     while (!cur.fast && ++t < t_end) cur = cursor.at(t);
-    if (!cur.fast) return;
+    if (!cur.fast) {  // no fast tile at all (the host lists the tiles that are not fast)
+        if (lane == 0) xcount[gw] = 0;
+        return;
+    }
     u32x4 x[kTileIters];
     // the word before the first tile (tile 0 of a stream has none: key 0 is masked)
     uint32_t prev_word = ld_u32(cur.base + 4 * cur.j0 - (cur.j0 ? 4 : 0));
@@ -555,6 +569,8 @@ __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restri
         const uint64_t cmask = __ballot(cand);
         const bool tie = __any(cand && first != last);
         const uint32_t win = 0xffffu - (p & 0xffffu);
+        if (lane == 0) xlist[t_begin + n_ties] = (uint32_t)t;  // kept only if it is a tie
+        n_ties += tie ? 1u : 0u;
         pend_t = t;
         pend_j0 = cur.j0;
         pend_mask = tie ? 0 : cmask;
@@ -585,6 +601,7 @@ __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restri
         if (lane == 0) {
             rec[pend_t].key = bk;
             rec[pend_t].j = bj;
+            xcount[gw] = n_ties;
         }
     }
 }
@@ -615,43 +632,43 @@ __device__ __forceinline__ void exact_tile(const uint64_t *tl, const uint64_t *t
     }
 }
 
-// Exact tiles, one wave per item, grid-strided: items 0 .. 2n-1 are tile 0 and the last tile
-// of every stream when the fast kernel could not take them (tile_fast: the stream ends inside
-// the tile); the rest sweep the records in 64-record chunks for the tiles the fast kernel
-// marked (kTieMark) and recompute those over the same key range (tile_key_end).
+// Exact tiles, one wave per item, grid-strided: items 0 .. n_waves - 1 are the tie lists of
+// the tile kernel's waves (xlist / xcount), the rest the host's list of tiles the fast path
+// does not take (tile_fast: the stream ends inside the tile; d.xtiles).  Each is recomputed
+// over the same key range the fast path would have covered (tile_key_end).
 __global__ __launch_bounds__(256) void rc_edge_kernel(const KeyTables *__restrict__ tab,
                                                       StreamDesc d, uint64_t n_streams,
                                                       uint64_t n_tiles,
                                                       TileRecord *__restrict__ rec,
-                                                      uint64_t *__restrict__ gmax) {
+                                                      uint64_t *__restrict__ gmax,
+                                                      const uint32_t *__restrict__ xlist,
+                                                      const uint32_t *__restrict__ xcount,
+                                                      uint64_t n_waves) {
     __shared__ __attribute__((aligned(16))) uint64_t s_full[2048];
+    const uint64_t gw = (uint64_t)blockIdx.x * (blockDim.x >> 6) +
+                        __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    const uint64_t n_host = sload(d.xtiles);
+    // almost every workgroup has nothing to recompute: it leaves before staging the tables
+    bool work = false;
+    for (uint64_t e = gw; e < n_waves + n_host && !work; e += nw)
+        work = e >= n_waves || __builtin_amdgcn_readfirstlane(xcount[e]) != 0;
+    if (!__syncthreads_or(work)) return;
     const uint64_t *gfull = &tab->tl[0][0];
     for (uint32_t i = threadIdx.x; i < 2048u; i += blockDim.x) s_full[i] = gfull[i];
     __syncthreads();
     const uint64_t *tl = s_full, *th = s_full + 1024;
-    const uint64_t gw = (uint64_t)blockIdx.x * (blockDim.x >> 6) +
-                        __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    const uint64_t n_chunks = (n_tiles + 63) / 64;
-    for (uint64_t e = gw; e < 2 * n_streams + n_chunks; e += nw) {
-        if (e < 2 * n_streams) {
-            const uint64_t s = e >> 1;
-            const uint64_t tb = sload(d.tile_base + s), nt = sload(d.tile_base + s + 1) - tb;
-            if (nt == 0) continue;
-            uint64_t t = tb;
-            if (e & 1) {  // the last tile, unless it is tile 0
-                if (nt < 2) continue;
-                t = tb + nt - 1;
+    for (uint64_t e = gw; e < n_waves + n_host; e += nw) {
+        if (e < n_waves) {
+            const uint64_t t0 = n_tiles * e / n_waves;
+            const uint32_t c = (uint32_t)__builtin_amdgcn_readfirstlane(xcount[e]);
+            for (uint32_t i = 0; i < c; ++i) {
+                const uint64_t t = (uint32_t)__builtin_amdgcn_readfirstlane(xlist[t0 + i]);
+                exact_tile(tl, th, d, stream_of_tile(d, n_streams, t), t, rec, gmax);
             }
-            if (tile_fast((t - tb) * kTileKeys, sload(d.len + s))) continue;
-            exact_tile(tl, th, d, s, t, rec, gmax);
         } else {
-            const uint64_t t0 = (e - 2 * n_streams) * 64, t = t0 + lane_id();
-            const bool marked = t < n_tiles && rec[t].j == kTieMark;
-            for (uint64_t m = __ballot(marked); m; m &= m - 1) {
-                const uint64_t tm = t0 + __builtin_ctzll(m);
-                exact_tile(tl, th, d, stream_of_tile(d, n_streams, tm), tm, rec, gmax);
-            }
+            const uint64_t t = sload(d.xtiles + 1 + (e - n_waves));
+            exact_tile(tl, th, d, stream_of_tile(d, n_streams, t), t, rec, gmax);
         }
     }
 }
@@ -1654,18 +1671,36 @@ __global__ __launch_bounds__(256) void rc_join_kernel(const KeyTables *__restric
 // access pattern -- persistent 1024-thread workgroups, each wave reading 16 KiB tiles through
 // a 16-slot register ring of 16-byte nontemporal loads -- and XORs them.  Its rate is the
 // streaming-read ceiling the tile kernel is compared against on the same box.
+//
+// block > 0 (diagnostics: the tile order): instead of one contiguous range per wave, the waves
+// take runs of `block` consecutive tiles in turn (wave w: runs w, w + nw, ...), so at any moment
+// the whole grid reads one window of nw * block tiles -- far fewer distinct pages in flight.
+__device__ __forceinline__ uint64_t probe_tile(uint64_t k, uint64_t gw, uint64_t nw,
+                                               uint64_t block) {
+    return (k / block * nw + gw) * block + k % block;  // the k-th tile of wave gw
+}
+
 __global__ __launch_bounds__(1024) void rc_read_probe_kernel(const uint8_t *__restrict__ src,
                                                              uint64_t n_tiles,
-                                                             uint32_t *__restrict__ out) {
+                                                             uint32_t *__restrict__ out,
+                                                             uint64_t block) {
     const uint32_t lane = lane_id();
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t gw = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
     const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    uint64_t t = n_tiles * gw / nw;
-    const uint64_t t_end = n_tiles * (gw + 1) / nw;
+    uint64_t t, t_end;
+    if (block == 0) {
+        t = n_tiles * gw / nw;
+        t_end = n_tiles * (gw + 1) / nw;
+    } else {  // k-th tile of this wave; tiles past n_tiles are dropped
+        t = 0;
+        t_end = 0;
+        while (probe_tile(t_end, gw, nw, block) < n_tiles) ++t_end;  // short: n_tiles / nw
+    }
     if (t >= t_end) return;
+    auto tile_of = [&](uint64_t k) { return block == 0 ? k : probe_tile(k, gw, nw, block); };
     u32x4 x[kTileIters];
-    gu32x4 *p = as_global_x4(src + t * (uint64_t)kTileKeys * 4) + lane;
+    gu32x4 *p = as_global_x4(src + tile_of(t) * (uint64_t)kTileKeys * 4) + lane;
 #pragma unroll
     for (int it = 0; it < kTileIters; ++it) {
         x[it] = RC_STREAM_LOAD(p + it * 64);
@@ -1674,7 +1709,7 @@ __global__ __launch_bounds__(1024) void rc_read_probe_kernel(const uint8_t *__re
     uint32_t acc = 0;
     for (; t < t_end; ++t) {
         const uint64_t tn = t + 1 < t_end ? t + 1 : t;
-        gu32x4 *q = as_global_x4(src + tn * (uint64_t)kTileKeys * 4) + lane;
+        gu32x4 *q = as_global_x4(src + tile_of(tn) * (uint64_t)kTileKeys * 4) + lane;
 #pragma unroll
         for (int it = 0; it < kTileIters; ++it) {
             const u32x4 w = x[it];
@@ -1754,8 +1789,8 @@ int rc_diag_read(uint64_t *out, uint32_t cap, uint32_t *n) {
 #endif
 
 int rc_launch_tiles(const KeyTables *d_tables, StreamDesc desc, uint64_t n_streams,
-                    uint64_t n_tiles, TileRecord *d_records, uint64_t *d_gmax, void *stream,
-                    void *mid_event) {
+                    uint64_t n_tiles, TileRecord *d_records, uint64_t *d_gmax,
+                    uint32_t *d_xlist, void *stream, void *mid_event) {
     hipStream_t st = (hipStream_t)stream;
     if (n_tiles == 0) {
         if (mid_event && hipEventRecord((hipEvent_t)mid_event, st) != hipSuccess) return 1;
@@ -1765,23 +1800,28 @@ int rc_launch_tiles(const KeyTables *d_tables, StreamDesc desc, uint64_t n_strea
     uint64_t grid = (n_tiles + waves_per_wg - 1) / waves_per_wg;
     const uint64_t cus = (uint64_t)cu_count();
     if (grid > cus) grid = cus;  // persistent: one 144 KiB-LDS workgroup per CU
+    // the tie lists: n_tiles slots, then one count per wave
+    uint32_t *d_xcount = d_xlist + n_tiles;
+    const uint64_t n_waves = grid * waves_per_wg;
     if (d_gmax)
         hipLaunchKernelGGL(rc_tile_kernel<kTileGroups>, dim3((unsigned)grid), dim3(1024), 0, st,
-                           d_tables, desc, n_streams, n_tiles, d_records, d_gmax);
+                           d_tables, desc, n_streams, n_tiles, d_records, d_gmax, d_xlist,
+                           d_xcount);
     else
         hipLaunchKernelGGL(rc_tile_kernel<1>, dim3((unsigned)grid), dim3(1024), 0, st, d_tables,
-                           desc, n_streams, n_tiles, d_records, d_gmax);
+                           desc, n_streams, n_tiles, d_records, d_gmax, d_xlist, d_xcount);
     if (launch_status("rc_tile_kernel")) return 1;
     if (mid_event && hipEventRecord((hipEvent_t)mid_event, st) != hipSuccess) {
         snprintf(g_launch_err, sizeof g_launch_err, "hipEventRecord failed");
         return 1;
     }
-    // edge tiles (2 per stream) + the marked-tile sweep (64 records per item), one wave each
-    uint64_t egrid = (2 * n_streams + (n_tiles + 63) / 64 + 3) / 4;
+    // one wave per tie list (almost always empty) and per host-listed tile, grid-strided
+    uint64_t egrid = (n_waves + 3) / 4;
     if (egrid > 4 * cus) egrid = 4 * cus;
     if (egrid == 0) egrid = 1;
     hipLaunchKernelGGL(rc_edge_kernel, dim3((unsigned)egrid), dim3(256), 0, st, d_tables, desc,
-                       n_streams, n_tiles, d_records, d_gmax);
+                       n_streams, n_tiles, d_records, d_gmax, (const uint32_t *)d_xlist,
+                       (const uint32_t *)d_xcount, n_waves);
     return launch_status("rc_edge_kernel");
 }
 
@@ -1849,8 +1889,10 @@ int rc_launch_read_probe(const uint8_t *d_src, uint64_t nbytes, uint32_t *d_out,
     uint64_t grid = (n_tiles + 15) / 16;
     const uint64_t cus = (uint64_t)cu_count();
     if (grid > cus) grid = cus;
+    uint64_t block = 0;  // RC_PROBE_BLOCK (diagnostics): interleaved runs of tiles
+    if (const char *e = getenv("RC_PROBE_BLOCK")) block = strtoull(e, nullptr, 0);
     hipLaunchKernelGGL(rc_read_probe_kernel, dim3((unsigned)grid), dim3(1024), 0,
-                       (hipStream_t)stream, d_src, n_tiles, d_out);
+                       (hipStream_t)stream, d_src, n_tiles, d_out, block);
     return launch_status("rc_read_probe_kernel");
 }
 

@@ -9,7 +9,8 @@ export TMPDIR=/tmp
 B=${B:-replicat_amd/diag_head.so}
 for r in $(seq ${ROUNDS:-3}); do
   for cfg in ${CONFIGS:-2 3iii}; do
-    for v in new old; do
+    order="new old"; [ $((r % 2)) -eq 0 ] && order="old new"   # alternate which runs first
+    for v in $order; do
       if [ $v = old ]; then export RC_LIB_PATH=$B; else unset RC_LIB_PATH; fi
       timeout -k 10 300 python -u bench.py --config $cfg --steps 10 --warmup 2 --cpu-streams 0 --no-verify > $out/${v}_${cfg}_$r.log 2>&1 \
         || { echo "bench $v $cfg failed"; tail -n 5 $out/${v}_${cfg}_$r.log; exit 4; }
