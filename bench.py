@@ -626,12 +626,18 @@ def main(argv=None, backend=Backend):
     cuts = be.zeros_i64(total_cap)
     counts = be.zeros_i64(n)
     be.synchronize()
+    # the stream arrays as the C ABI takes them (u64), built once: converting 65,536-entry
+    # Python lists on every call is host time the device would wait for
+    if long is None:
+        ptrs_a = np.ascontiguousarray(ptrs, dtype=np.uint64)
+        lens_a = np.ascontiguousarray(lens, dtype=np.uint64)
+        last_a = np.ascontiguousarray(last if last is not None else np.zeros(n), dtype=np.uint64)
 
     def step():
         if long is not None:
             long.step()
         else:
-            ch.chunk_device(ptrs, lens, last, cuts.data_ptr(), counts.data_ptr(), hs)
+            ch.chunk_device(ptrs_a, lens_a, last_a, cuts.data_ptr(), counts.data_ptr(), hs)
 
     for _ in range(args.warmup):
         step()

@@ -363,19 +363,24 @@ int stage_descriptors(rc_chunker *ch, Workspace &ws, uint64_t n, const uint8_t *
     return 0;
 }
 
-uint64_t *group_maxima(Workspace &ws, const Plan &plan) {
-    return reinterpret_cast<uint64_t *>(static_cast<char *>(ws.d_records.p) +
-                                        (plan.n_tiles + 1) * sizeof(TileRecord));
+GroupRecord *group_records(Workspace &ws, const Plan &plan) {
+    return reinterpret_cast<GroupRecord *>(static_cast<char *>(ws.d_records.p) +
+                                           (plan.n_tiles + 1) * sizeof(TileRecord));
 }
 
 // the tile kernel's per-wave tie lists: n_tiles slots + one count per wave (<= n_tiles + 16)
 uint32_t *tie_lists(Workspace &ws, const Plan &plan) {
-    return reinterpret_cast<uint32_t *>(group_maxima(ws, plan) + plan.n_tiles + 1);
+    return reinterpret_cast<uint32_t *>(group_records(ws, plan) + plan.n_tiles + 1);
 }
 
 size_t records_bytes(const Plan &plan) {
-    return (plan.n_tiles + 1) * (sizeof(TileRecord) + 8) + (2 * plan.n_tiles + 32) * 4;
+    return (plan.n_tiles + 1) * (sizeof(TileRecord) + sizeof(GroupRecord)) +
+           (2 * plan.n_tiles + 32) * 4;
 }
+
+// batches of at least this many streams walk their chains one lane per stream (when the
+// windows are small and every stream is one segment: kernels.hip rc_lane_chain_kernel)
+constexpr uint64_t kLaneMinStreams = 256;
 
 int upload_and_launch(rc_chunker *ch, Workspace &ws, const Plan &plan, ChainParams prm,
                       uint64_t *d_cuts, int64_t *d_counts, hipStream_t stream) {
@@ -407,12 +412,19 @@ int upload_and_launch(rc_chunker *ch, Workspace &ws, const Plan &plan, ChainPara
         }
         HIP_TRY(hipEventRecord(ev[0], stream));
     }
-    uint64_t *gmax = ch->groups ? group_maxima(ws, plan) : nullptr;
-    prm.gmax = gmax;
+    GroupRecord *grp = ch->groups ? group_records(ws, plan) : nullptr;
+    prm.grp = grp;
+    prm.n_tiles = plan.n_tiles;
+    // lane-per-stream chain (kernels.hip rc_lane_chain_kernel) for batches of many streams;
+    // RC_LANE_CHAIN=0 never, =1 whatever the count (read per call: tests switch it)
+    {
+        const char *e = getenv("RC_LANE_CHAIN");
+        prm.lane = e && e[0] == '0' ? 0u : (e && e[0] == '1') ? 2u : plan.n >= kLaneMinStreams ? 1u : 0u;
+    }
     // 32-bit chain steps: small windows (the one-row record cache) and key indices < 2^32
     prm.lean = ch->small && plan.max_len < (16ull << 30) ? 1u : 0u;
     if (rc_launch_tiles(ch->d_tables, d, plan.n, plan.n_tiles,
-                        static_cast<TileRecord *>(ws.d_records.p), gmax, tie_lists(ws, plan),
+                        static_cast<TileRecord *>(ws.d_records.p), grp, tie_lists(ws, plan),
                         stream, ch->timing ? ev[1] : nullptr))
         return fail(RC_ERR_HIP, "%s", rc_launch_error());
     if (ch->timing) HIP_TRY(hipEventRecord(ev[2], stream));
@@ -441,8 +453,10 @@ ChainParams chain_params(const rc_chunker *ch, const Plan &plan, uint64_t max_st
     p.seg_bytes = plan.seg_bytes;
     p.seg_cap = plan.seg_cap;
     p.ext_steps = ch->ext_steps;
-    p.gmax = nullptr;  // set per launch (upload_and_launch)
+    p.grp = nullptr;  // set per launch (upload_and_launch)
+    p.n_tiles = 0;
     p.lean = 0;
+    p.lane = 0;
     return p;
 }
 
@@ -801,7 +815,8 @@ uint64_t rc_tile_keys(void) { return kTileKeys; }
 
 int rc_tile_records(rc_chunker *ch, uint64_t n, const uint8_t *const *d_streams,
                     const uint64_t *lens, const uint64_t *last_piece, uint64_t *keys,
-                    uint64_t *js, uint64_t *gmax, uint64_t cap, uint64_t *n_tiles) {
+                    uint64_t *js, uint64_t *gmax, uint64_t *gsec, uint64_t cap,
+                    uint64_t *n_tiles) {
     if (!ch || !n_tiles) return fail(RC_ERR_ARGUMENT, "null argument");
     if (int rc = validate_streams(n, d_streams, lens, last_piece, true)) return rc;
     std::lock_guard<std::mutex> lock(ch->mu);
@@ -812,24 +827,26 @@ int rc_tile_records(rc_chunker *ch, uint64_t n, const uint8_t *const *d_streams,
     if (int rc = ws.d_desc.ensure(plan.bytes)) return rc;
     if (int rc = ws.d_records.ensure(records_bytes(plan))) return rc;
     HIP_TRY(hipMemcpy(ws.d_desc.p, ws.h_desc.p, plan.bytes, hipMemcpyHostToDevice));
-    uint64_t *d_gmax = ch->groups ? group_maxima(ws, plan) : nullptr;
+    GroupRecord *d_grp = ch->groups ? group_records(ws, plan) : nullptr;
     if (rc_launch_tiles(ch->d_tables, desc_view(ws.d_desc.p, n), n, plan.n_tiles,
-                        static_cast<TileRecord *>(ws.d_records.p), d_gmax, tie_lists(ws, plan),
+                        static_cast<TileRecord *>(ws.d_records.p), d_grp, tie_lists(ws, plan),
                         nullptr, nullptr))
         return fail(RC_ERR_HIP, "%s", rc_launch_error());
     HIP_TRY(hipDeviceSynchronize());
     std::vector<TileRecord> h(plan.n_tiles);
-    std::vector<uint64_t> hg(plan.n_tiles, ~0ull);
+    std::vector<GroupRecord> hg(plan.n_tiles, GroupRecord{~0ull, 0ull});
     if (plan.n_tiles) {
         HIP_TRY(hipMemcpy(h.data(), ws.d_records.p, plan.n_tiles * sizeof(TileRecord),
                           hipMemcpyDeviceToHost));
-        if (d_gmax) HIP_TRY(hipMemcpy(hg.data(), d_gmax, plan.n_tiles * 8, hipMemcpyDeviceToHost));
+        if (d_grp)
+            HIP_TRY(hipMemcpy(hg.data(), d_grp, plan.n_tiles * sizeof(GroupRecord), hipMemcpyDeviceToHost));
     }
     *n_tiles = plan.n_tiles;
     for (uint64_t t = 0; t < plan.n_tiles && t < cap; ++t) {
         keys[t] = h[t].key;
         js[t] = h[t].j;
-        if (gmax) gmax[t] = hg[t];
+        if (gmax) gmax[t] = hg[t].max;
+        if (gsec) gsec[t] = hg[t].sec;
     }
     return RC_OK;
 }

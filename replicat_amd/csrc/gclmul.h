@@ -65,6 +65,26 @@ struct TileRecord {
     uint64_t j;
 };
 
+// Per-tile group bounds of the small-window tile kernel (kTileGroups groups of kGroupKeys keys;
+// group g = the tile kernel's iterations g*kTileIters/G .., in which lane l holds keys
+// 256*it + 4l .. 256*it + 4l + 3):
+//   max: u16 g = the top-16 maximum of group g (keys that do not exist count as 0);
+//   sec: u16 g = min(0xffff - B, 1023) << 6 | l, with l the lowest lane whose own top-16
+//        maximum in the group equals the group's, and B the top-16 maximum over every OTHER
+//        lane's keys of the group -- so every key of the group outside lane l has
+//        top16 <= 0xffff - (sec_g >> 6) = max(B, 0xfc00).  (Exact near the top, where the
+//        chain's thresholds lie: the maximum of ~1000 keys is within 1023 of 0xffff.)
+// A tile computed exactly (rc_edge_kernel) has max = ~0 and sec = 0: no bound at all.
+struct GroupRecord {
+    uint64_t max;
+    uint64_t sec;
+};
+__host__ __device__ inline uint32_t group_sec_field(uint32_t B, uint32_t lane) {
+    const uint32_t d = 0xffffu - B;
+    return (d < 1023u ? d : 1023u) << 6 | lane;
+}
+__host__ __device__ inline uint32_t group_sec_bound(uint32_t field) { return 0xffffu - (field >> 6); }
+
 struct ChainParams {
     uint64_t min_length;
     uint64_t max_length;
@@ -74,9 +94,11 @@ struct ChainParams {
     uint64_t seg_bytes;   // chain segment length (multiple of 4)
     uint64_t seg_cap;     // entries per speculative list
     uint64_t ext_steps;   // steps a speculative chain runs past its segment end
-    const uint64_t *gmax; // per-tile group maxima (rc_launch_tiles), or NULL
+    const GroupRecord *grp;  // per-tile group bounds (rc_launch_tiles), or NULL
+    uint64_t n_tiles;     // tiles of the call (records and group bounds hold n_tiles + 1)
     uint32_t open;        // RC_OPEN: non-final prefix, no tail rule
     uint32_t lean;        // small windows and every stream < 16 GiB: 32-bit chain steps
+    uint32_t lane;        // lane-per-stream chain allowed (rc_lane_chain_kernel; 2 = forced)
 };
 
 // splitmix64 finaliser (replicat_amd/synth.py)
@@ -92,13 +114,13 @@ __host__ __device__ inline uint64_t splitmix64(uint64_t x) {
 // Launchers implemented in kernels.hip (host-callable, enqueue only).
 extern "C" {
 // d_records: n_tiles + 1 entries (the last is scratch for the tile kernel's pipeline)
-// d_gmax (may be NULL): n_tiles + 1 words of per-group top-16 maxima (kTileGroups x u16 per
-// tile) -- the chain's bounds for small windows.  mid_event (a hipEvent_t, may be NULL):
+// d_grp (may be NULL): n_tiles + 1 group records (per-group top-16 bounds, GroupRecord) --
+// the chain's bounds for small windows.  mid_event (a hipEvent_t, may be NULL):
 // recorded between the tile and the edge kernel.
 // d_xlist: n_tiles + (one count per tile-kernel wave: at most n_tiles) u32 of scratch for the
 // tile kernel's per-wave tie lists.
 int rc_launch_tiles(const rc::KeyTables *d_tables, rc::StreamDesc desc, uint64_t n_streams,
-                    uint64_t n_tiles, rc::TileRecord *d_records, uint64_t *d_gmax,
+                    uint64_t n_tiles, rc::TileRecord *d_records, rc::GroupRecord *d_grp,
                     uint32_t *d_xlist, void *stream, void *mid_event);
 int rc_launch_chain(const rc::KeyTables *d_tables, rc::StreamDesc desc, uint64_t n_streams,
                     rc::ChainParams prm, uint64_t n_segs, const rc::TileRecord *d_records,

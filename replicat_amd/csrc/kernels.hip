@@ -459,10 +459,35 @@ __device__ __forceinline__ void stage_tile_tables(const KeyTables *tab) {
     __syncthreads();
 }
 
+// Group bounds of one tile from the lanes' packed per-group top-16 maxima (gpk: group 2i in the
+// low half of gpk[i], 2i + 1 in the high half): the group maxima, and per group the lowest lane
+// holding its maximum together with the maximum over every other lane (GroupRecord).  Two
+// packed wave maxima per pair of groups; the lanes come from ballots (SALU).
+template <int G>
+__device__ __forceinline__ GroupRecord tile_groups(const uint32_t (&gpk)[(G + 1) / 2]) {
+    const uint32_t lane = lane_id();
+    uint64_t gm = 0, gs = 0;
+#pragma unroll
+    for (int i = 0; i < (G + 1) / 2; ++i) {
+        const uint32_t v = gpk[i];
+        const uint32_t mx = wave_max_pk16(v);
+        // every lane is live in the tile kernel, so each maximum is some lane's
+        const uint32_t l0 = (uint32_t)__builtin_ctzll(__ballot((v & 0xffffu) == (mx & 0xffffu)));
+        const uint32_t l1 = (uint32_t)__builtin_ctzll(__ballot((v >> 16) == (mx >> 16)));
+        const uint32_t keep = (lane == l0 ? 0u : 0xffffu) | (lane == l1 ? 0u : 0xffff0000u);
+        const uint32_t sec = wave_max_pk16(v & keep);
+        gm |= (uint64_t)mx << (32 * i);
+        const uint32_t f = group_sec_field(sec & 0xffffu, l0) | group_sec_field(sec >> 16, l1) << 16;
+        gs |= (uint64_t)f << (32 * i);
+    }
+    return GroupRecord{gm, gs};
+}
+
 // Persistent: one 1024-thread workgroup per CU, each wave a contiguous range of tiles.
-// G > 1: also gmax[t] = the top-16 maximum of each of the tile's G key groups (u16 g at bits
-// 16g; keys that do not exist count as 0), an upper bound the chain uses to leave most of an
-// edge range unscanned (chain_step).
+// G > 1: also grp[t] = the tile's group bounds (GroupRecord: the top-16 maximum of each of its
+// G key groups, keys that do not exist counting as 0, and the maximum outside the lane holding
+// it), upper bounds the chains use to leave most of an edge range unscanned (chain_step,
+// rc_lane_chain_kernel).
 //
 // Tiles the fast path cannot settle -- a candidate lane holding its top-16 maximum twice --
 // are listed per wave for the edge kernel: xlist[t_begin + i] (i < xcount[wave]).  Every tile
@@ -473,7 +498,7 @@ __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restri
                                                        StreamDesc d, uint64_t n_streams,
                                                        uint64_t n_tiles,
                                                        TileRecord *__restrict__ rec,
-                                                       uint64_t *__restrict__ gmax,
+                                                       GroupRecord *__restrict__ grp,
                                                        uint32_t *__restrict__ xlist,
                                                        uint32_t *__restrict__ xcount) {
     stage_tile_tables(tab);
@@ -532,11 +557,9 @@ __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restri
         uint32_t top, first, last;
         uint32_t gpk[(G + 1) / 2];
         tile_scan<G>(cur, nx, x, prev_word, lb_a, lb_b, top, first, last, gpk);
-        if constexpr (G > 1) {  // this tile's group maxima, stored now (no exact key needed)
-            uint64_t gm = 0;
-#pragma unroll
-            for (int i = 0; i < (G + 1) / 2; ++i) gm |= (uint64_t)wave_max_pk16(gpk[i]) << (32 * i);
-            if (lane == 0) gmax[t] = gm;
+        if constexpr (G > 1) {  // this tile's group bounds, stored now (no exact key needed)
+            const GroupRecord g = tile_groups<G>(gpk);
+            if (lane == 0) grp[t] = g;
         }
 
         // retire the pending tile: (first maximal exact key, index) over its candidate lanes
@@ -619,7 +642,7 @@ __device__ __forceinline__ uint64_t stream_of_tile(const StreamDesc &d, uint64_t
 
 __device__ __forceinline__ void exact_tile(const uint64_t *tl, const uint64_t *th,
                                            const StreamDesc &d, uint64_t s, uint64_t t,
-                                           TileRecord *rec, uint64_t *gmax) {
+                                           TileRecord *rec, GroupRecord *grp) {
     const uint64_t j0 = (t - sload(d.tile_base + s)) * kTileKeys;
     const uint64_t jb = tile_key_end(j0, sload(d.len + s), sload(d.jneed + s));
     uint64_t bk = 0, bj = ~0ull;
@@ -628,7 +651,7 @@ __device__ __forceinline__ void exact_tile(const uint64_t *tl, const uint64_t *t
     if (lane_id() == 0) {
         rec[t].key = bk;
         rec[t].j = bj;
-        if (gmax) gmax[t] = ~0ull;  // no group bounds for an exact tile: the chain scans
+        if (grp) grp[t] = GroupRecord{~0ull, 0ull};  // no group bounds for an exact tile
     }
 }
 
@@ -640,7 +663,7 @@ __global__ __launch_bounds__(256) void rc_edge_kernel(const KeyTables *__restric
                                                       StreamDesc d, uint64_t n_streams,
                                                       uint64_t n_tiles,
                                                       TileRecord *__restrict__ rec,
-                                                      uint64_t *__restrict__ gmax,
+                                                      GroupRecord *__restrict__ grp,
                                                       const uint32_t *__restrict__ xlist,
                                                       const uint32_t *__restrict__ xcount,
                                                       uint64_t n_waves) {
@@ -664,11 +687,11 @@ __global__ __launch_bounds__(256) void rc_edge_kernel(const KeyTables *__restric
             const uint32_t c = (uint32_t)__builtin_amdgcn_readfirstlane(xcount[e]);
             for (uint32_t i = 0; i < c; ++i) {
                 const uint64_t t = (uint32_t)__builtin_amdgcn_readfirstlane(xlist[t0 + i]);
-                exact_tile(tl, th, d, stream_of_tile(d, n_streams, t), t, rec, gmax);
+                exact_tile(tl, th, d, stream_of_tile(d, n_streams, t), t, rec, grp);
             }
         } else {
             const uint64_t t = sload(d.xtiles + 1 + (e - n_waves));
-            exact_tile(tl, th, d, stream_of_tile(d, n_streams, t), t, rec, gmax);
+            exact_tile(tl, th, d, stream_of_tile(d, n_streams, t), t, rec, grp);
         }
     }
 }
@@ -856,7 +879,7 @@ struct RecCache {
     uint64_t g[R];           // group maxima of the same tiles (when the tile kernel made them)
 
     __device__ bool has(uint64_t t) const { return t >= c0 && t - c0 < n; }
-    __device__ void load(const TileRecord *rec, const uint64_t *gmax, const ChainStream &st,
+    __device__ void load(const TileRecord *rec, const GroupRecord *grp, const ChainStream &st,
                          uint64_t lo) {
         c0 = (uint32_t)lo;
         n = (uint32_t)min(st.nt - lo, (uint64_t)64 * R);
@@ -866,7 +889,7 @@ struct RecCache {
             if ((uint64_t)64 * u < n) {
                 const uint64_t t = st.tb0 + lo + min((uint64_t)64 * u + lane, n - 1);
                 v[u] = rec[t];
-                if (gmax) g[u] = gmax[t];
+                if (grp) g[u] = grp[t].max;
             }
     }
     __device__ TileRecord get(uint64_t t, uint64_t &gm) const {  // t uniform and cached
@@ -971,7 +994,7 @@ __device__ int chain_step(const uint64_t *tl, const uint64_t *th, const uint32_t
                 need_hi = max(need_hi, te1);
             }
             if (need_lo <= need_hi && !(cache.has(need_lo) && cache.has(need_hi)))
-                cache.load(rec, prm.gmax, st, need_lo);  // one round trip, edge records included
+                cache.load(rec, prm.grp, st, need_lo);  // one round trip, edge records included
             // edge tiles past the span (windows wider than 64R tiles) come from memory, issued
             // together with the reload
             TileRecord er0 = {}, er1 = {};
@@ -979,11 +1002,11 @@ __device__ int chain_step(const uint64_t *tl, const uint64_t *th, const uint32_t
             const bool g0 = one0 && !cache.has(te0), g1 = one1 && !cache.has(te1);
             if (g0) {
                 er0 = rec[st.tb0 + te0];
-                if (prm.gmax) gm0 = prm.gmax[st.tb0 + te0];
+                if (prm.grp) gm0 = prm.grp[st.tb0 + te0].max;
             }
             if (g1) {
                 er1 = rec[st.tb0 + te1];
-                if (prm.gmax) gm1 = prm.gmax[st.tb0 + te1];
+                if (prm.grp) gm1 = prm.grp[st.tb0 + te1].max;
             }
             if (have_rec) {
                 cache.reduce(t_lo, t_hi, bk, bj);
@@ -1010,7 +1033,7 @@ __device__ int chain_step(const uint64_t *tl, const uint64_t *th, const uint32_t
             // scan is trimmed to its groups from the first to the last one that can.  The head
             // tile always holds the previous cut's key -- the maximum of the previous window --
             // so its record rarely settles the head; its groups after that key usually do.
-            if (prm.gmax) {
+            if (prm.grp) {
                 const uint32_t tb16 = (uint32_t)(bk >> 48);
                 if (one0 && r0.live && trim_groups(gm0, te0, tb16, a0, b0))
                     r0.init(st.base, st.L / 4 - 1, a0, b0, 0);
@@ -1158,7 +1181,7 @@ __device__ int chain_step_small(const uint64_t *tl, const uint64_t *th, const ui
                 need_hi = max(need_hi, te1);
             }
             if (need_lo <= need_hi && !(cache.has(need_lo) && cache.has(need_hi)))
-                cache.load(rec, prm.gmax, st, need_lo);  // covers them all: window + 2 <= 64 tiles
+                cache.load(rec, prm.grp, st, need_lo);  // covers them all: window + 2 <= 64 tiles
             const uint32_t lane = lane_id();
             const uint64_t key = cache.v[0].key;
             // the full tiles' best record: the lanes' key high words, then (on a tie) the low
@@ -1187,13 +1210,13 @@ __device__ int chain_step_small(const uint64_t *tl, const uint64_t *th, const ui
                 const int l = (int)(te0 - cache.c0);
                 ek0 = lane_u64(key, l);
                 ej0 = (uint32_t)__builtin_amdgcn_readlane((uint32_t)cache.v[0].j, l);
-                if (prm.gmax) gm0 = lane_u64(cache.g[0], l);
+                if (prm.grp) gm0 = lane_u64(cache.g[0], l);
             }
             if (one1) {
                 const int l = (int)(te1 - cache.c0);
                 ek1 = lane_u64(key, l);
                 ej1 = (uint32_t)__builtin_amdgcn_readlane((uint32_t)cache.v[0].j, l);
-                if (prm.gmax) gm1 = lane_u64(cache.g[0], l);
+                if (prm.grp) gm1 = lane_u64(cache.g[0], l);
             }
             // settle the edge ranges by their tiles' records, then trim them by the group
             // maxima (chain_step explains both rules)
@@ -1206,7 +1229,7 @@ __device__ int chain_step_small(const uint64_t *tl, const uint64_t *th, const ui
                 if (ek1 != 0 && ej1 >= a1 && ej1 <= b1) take_best32(ek1, ej1, bk, bj);
                 live1 = false;
             }
-            if (prm.gmax) {
+            if (prm.grp) {
                 const uint32_t tb16 = (uint32_t)(bk >> 48);
                 if (one0 && live0) {
                     trim_groups32(gm0, te0, tb16, a0, b0);
@@ -1384,6 +1407,323 @@ __global__ __launch_bounds__(kChainWaves * 64) void rc_spec_kernel(const KeyTabl
         if (direct) counts[s] = overflow ? -1 : (int64_t)n;
         else seg_counts[q] = overflow ? ~0ull : (n | (term ? (1ull << 63) : 0));
     }
+}
+
+// ---- the lane-per-stream chain (small windows, many single-segment streams)
+//
+// rc_spec_kernel walks one stream per WAVE: a step's decisions are scalar and its edge ranges
+// are scanned by the whole wave.  With 1 MiB streams and an 80 KB max_length (config 3 iii:
+// 65,536 streams x 22 steps) that is ~250 VALU + ~300 SALU per step and ~1.1 ms of a 13 ms
+// batch, almost all of it the scan of the head range -- the rest of the previous cut's group,
+// whose top-16 maximum is that cut's own key.  Here every LANE walks its own stream, and the
+// group bounds (GroupRecord) settle the edge ranges without a scan:
+//   * the window's full tiles come from their records (16-byte loads, all in flight together);
+//   * a partial edge range is settled by its tile's record when the record lies in it, or
+//     excluded when the record is below the best (head) or at most the best (tail) -- as in
+//     chain_step;
+//   * otherwise each group the range overlaps is excluded when its top-16 maximum is below
+//     the best so far; when only the maximum's own lane l0 can reach it (the other lanes'
+//     bound is below), the walking lane evaluates the keys of lane l0 in the range itself:
+//     kTileIters / G iterations of 4 keys, one 16-byte load and the word before each;
+//   * a group in which two lanes reach the bound (the window's maximum shares the previous
+//     cut's group: ~2 % of steps) is scanned exactly by the whole wave, lane after lane.
+// A key whose top 16 bits are below the best's cannot be >= it, so every rule is exact.
+constexpr int kLaneFull = 8;  // widest window of the lane chain: window keys / kTileKeys <= 8
+constexpr int kLaneIters = kTileIters / kTileGroups;  // tile-kernel iterations per group
+
+// Group classification of one edge range [a, b] inside tile te: bits of the groups whose lane-l0
+// keys are to be evaluated (ev) and of the groups left to an exact scan (sc).
+__device__ __forceinline__ void lane_groups(bool live, const GroupRecord &g, uint32_t te,
+                                            uint32_t a, uint32_t b, uint32_t t16, uint32_t &ev,
+                                            uint32_t &sc) {
+    ev = sc = 0;
+    if (!live) return;
+    const uint32_t tj0 = te * kTileKeys;
+    const uint32_t qa = (a - tj0) / kGroupKeys, qb = (b - tj0) / kGroupKeys;
+#pragma unroll
+    for (uint32_t q = 0; q < (uint32_t)kTileGroups; ++q) {
+        if (q < qa || q > qb) continue;
+        if (((uint32_t)(g.max >> (16 * q)) & 0xffffu) < t16) continue;  // nothing reaches the best
+        if (group_sec_bound((uint32_t)(g.sec >> (16 * q)) & 0xffffu) < t16) ev |= 1u << q;  // l0 only
+        else sc |= 1u << q;
+    }
+}
+
+// top-16 of key j from the prefilter entries of its two words (gclmul.h)
+__device__ __forceinline__ uint32_t top16_of(uint32_t e_lo_word, uint32_t e_hi_word) {
+    return ((e_lo_word & 0xffff0000u) ^ (e_hi_word << 16)) >> 16;
+}
+
+// One lane's keys in one group: keys jq + 256 i .. jq + 256 i + 3 (i < kLaneIters), jq =
+// the group's first key + 4 l -- one 16-byte block and the word before it per iteration.
+struct LaneQuarter {
+    uint32_t w[kLaneIters][5];  // the word before each block, then the block's 4 words
+};
+
+// Loads only the iterations holding a key of [a, b] (none when a > b).  A loaded block holds
+// a key <= b <= jmax, hence a stream byte: it cannot cross a page.
+__device__ __forceinline__ void lq_load(const uint8_t *base, uint32_t jq, uint32_t a, uint32_t b,
+                                        LaneQuarter &x) {
+#pragma unroll
+    for (int i = 0; i < kLaneIters; ++i) {
+        const uint32_t j4 = jq + 256 * i;
+        u32x4 v = u32x4{0u, 0u, 0u, 0u};
+        uint32_t p = 0;
+        if (j4 <= b && j4 + 3 >= a) {
+            v = *as_global_x4(base + 4ull * j4);
+            p = ld_u32(base + 4ull * j4 - (j4 ? 4 : 0));
+        }
+        x.w[i][0] = p;
+        x.w[i][1] = v.x;
+        x.w[i][2] = v.y;
+        x.w[i][3] = v.z;
+        x.w[i][4] = v.w;
+    }
+}
+
+// Folds the keys of x in [a, b] into (bk, bj): top-16 values from the compact prefilter, then
+// the exact key of the one with the largest top-16 value that reaches bk's -- a key with a
+// smaller top-16 value is smaller -- or, when two share it (rare), of every key exactly.
+__device__ __forceinline__ void lq_eval(const uint32_t *pf, const uint64_t *tl, const uint64_t *th,
+                                        const uint8_t *base, const LaneQuarter &x, uint32_t jq,
+                                        uint32_t a, uint32_t b, uint64_t &bk, uint32_t &bj) {
+    const uint32_t t16 = (uint32_t)(bk >> 48);
+    bool have = false, tie = false;
+    uint32_t ct = 0, cj = 0, clo = 0, chi = 0;
+#pragma unroll
+    for (int i = 0; i < kLaneIters; ++i) {
+        const uint32_t j4 = jq + 256 * i;
+        if (!(j4 <= b && j4 + 3 >= a)) continue;
+        const uint32_t *wd = x.w[i];
+        uint32_t e[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) e[k] = pfc_entry(pf, wd[k]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t j = j4 + k, t = top16_of(e[k], e[k + 1]);
+            if (j >= a && j <= b && t >= t16) {
+                if (!have || t > ct) {
+                    have = true;
+                    tie = false;
+                    ct = t;
+                    cj = j;
+                    clo = wd[k];
+                    chi = wd[k + 1];
+                } else if (t == ct) {
+                    tie = true;
+                }
+            }
+        }
+    }
+    if (have) take_best32(full_key(tl, th, clo, chi), cj, bk, bj);
+    if (tie) {  // every key of the lane in range, its words read again (rolled: rare, small code)
+#pragma unroll 1
+        for (uint32_t i = 0; i < 4 * kLaneIters; ++i) {
+            const uint32_t j = jq + 256 * (i >> 2) + (i & 3);
+            if (j >= a && j <= b)
+                take_best32(full_key(tl, th, ld_u32(base + 4ull * j - 4), ld_u32(base + 4ull * j)), j, bk, bj);
+        }
+    }
+}
+
+// Best exact key over [a, b] of one stream by the whole wave, 64 * U keys per memory round trip.
+template <int U>
+__device__ __forceinline__ void scan_range(const uint64_t *tl, const uint64_t *th,
+                                           const uint8_t *base, uint64_t a, uint64_t b,
+                                           uint64_t &bk, uint64_t &bj) {
+    const uint64_t lane = lane_id();
+    for (uint64_t r = a; r <= b; r += 64 * U) {
+        uint2 w[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t j = min(r + 64 * u + lane, b);
+            w[u].x = ld_u32(base + 4 * j - 4);
+            w[u].y = ld_u32(base + 4 * j);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t j = r + 64 * u + lane;
+            if (j <= b) take_best(full_key(tl, th, w[u].x, w[u].y), j, bk, bj);
+        }
+    }
+}
+
+template <int F>  // full tiles per window held in flight (window keys / kTileKeys <= F)
+__global__ __launch_bounds__(256) void rc_lane_chain_kernel(const KeyTables *__restrict__ tab,
+                                                            StreamDesc d, uint64_t n_streams,
+                                                            ChainParams prm,
+                                                            const TileRecord *__restrict__ rec,
+                                                            uint64_t *__restrict__ cuts,
+                                                            int64_t *__restrict__ counts) {
+    stage_chain_tables(tab);
+    const uint32_t *pf = s_chain_lds;
+    const uint64_t *full = reinterpret_cast<const uint64_t *>(s_chain_lds + 1024);
+    const uint64_t *tl = full, *th = full + 1024;
+    const uint32_t lane = lane_id();
+    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid - lane >= n_streams) return;  // the whole wave is past the last stream
+    const bool mine = gid < n_streams;
+    const uint64_t s = mine ? gid : n_streams - 1;  // surplus lanes shadow the last stream, silent
+    const GroupRecord *grp = prm.grp;
+    const uint8_t *base = d.ptr[s];
+    const uint64_t L = d.len[s], P = d.last[s];
+    const uint64_t tb0 = d.tile_base[s], nt = d.tile_base[s + 1] - tb0;
+    uint64_t *out = cuts + d.cut_base[s];
+    const uint64_t cap = d.cut_cap[s];
+    const uint32_t jmax = L >= 8 ? (uint32_t)((L - 4) / 4) : 0u;
+    const uint32_t minl = (uint32_t)prm.min_length, maxl = (uint32_t)prm.max_length;
+    const uint32_t T = (uint32_t)prm.window;
+    // a stream tile's global index; the spare record at n_tiles for anything else (a safe
+    // address for loads whose values are not used)
+    auto gtile = [&](bool use, uint32_t t) -> uint64_t { return use && t < nt ? tb0 + t : prm.n_tiles; };
+
+    uint64_t pos = 0, n = 0;
+    bool walking = mine && L > 0 && prm.max_steps > 0, overflow = false;
+    for (;;) {
+        if (!__any(walking)) break;
+        const uint64_t rem = L - pos;
+        const bool argmax = (P >= pos && P - pos >= maxl) || rem >= 2ull * maxl;
+        const uint32_t s4 = (uint32_t)(pos >> 2);
+        const uint32_t ja = s4 + 1, jb = min(s4 + T, jmax);
+        const bool win = walking && argmax && T > 0 && ja <= jb;
+        // full tiles [t_lo, t_hi); head [a0, b0] inside tile te0, tail [a1, b1] inside tile te1
+        const uint32_t t_lo = (ja + kTileKeys - 1) / kTileKeys, t_hi = (jb + 1) / kTileKeys;
+        const uint32_t nf = win && t_hi > t_lo ? t_hi - t_lo : 0u;
+        const uint32_t a0 = ja, b0 = min(jb, t_lo * kTileKeys - 1), te0 = ja / kTileKeys;
+        const uint32_t a1 = t_hi * kTileKeys, b1 = jb, te1 = t_hi;
+        bool live0 = win && ja < t_lo * kTileKeys;
+        bool live1 = win && t_hi >= t_lo && jb >= a1;
+
+        TileRecord fr[F];
+#pragma unroll
+        for (int i = 0; i < F; ++i) fr[i] = rec[gtile((uint32_t)i < nf, t_lo + i)];
+        const TileRecord r0 = rec[gtile(live0, te0)], r1 = rec[gtile(live1, te1)];
+        const GroupRecord g0 = grp[gtile(live0, te0)], g1 = grp[gtile(live1, te1)];
+        // with them, the words of the previous cut's lane in the rest of its group (key s4 is
+        // in tile te0 whenever the head range is not empty)
+        const bool spec = live0;
+        const uint32_t lc = (s4 & 255u) >> 2, qc = (s4 & (kTileKeys - 1)) / kGroupKeys;
+        const uint32_t jqc = (s4 & ~(uint32_t)(kGroupKeys - 1)) + 4 * lc;
+        LaneQuarter x0, x1;
+        lq_load(base, jqc, spec ? a0 : 1u, spec ? b0 : 0u, x0);
+
+        uint64_t bk = 0;
+        uint32_t bj = ~0u;
+#pragma unroll
+        for (int i = 0; i < F; ++i)
+            if ((uint32_t)i < nf && fr[i].key != 0) take_best32(fr[i].key, (uint32_t)fr[i].j, bk, bj);
+        if (live0) {
+            const uint32_t rj = (uint32_t)r0.j;
+            const bool inr = r0.key != 0 && rj >= a0 && rj <= b0;
+            if (inr) take_best32(r0.key, rj, bk, bj);
+            if (r0.key == 0 || inr || r0.key < bk) live0 = false;
+        }
+        if (live1) {
+            const uint32_t rj = (uint32_t)r1.j;
+            const bool inr = r1.key != 0 && rj >= a1 && rj <= b1;
+            if (inr) take_best32(r1.key, rj, bk, bj);
+            if (r1.key == 0 || inr || r1.key <= bk) live1 = false;
+        }
+        uint32_t ev0, sc0, ev1, sc1;
+        lane_groups(live0, g0, te0, a0, b0, (uint32_t)(bk >> 48), ev0, sc0);
+        lane_groups(live1, g1, te1, a1, b1, (uint32_t)(bk >> 48), ev1, sc1);
+
+        // groups handed to their lane l0, one of the head's and one of the tail's per round, the
+        // loads of both in flight together.  The head's first is, as a rule, the previous cut's
+        // own group and lane (that cut's key is the maximum of the previous window): its words
+        // came with the records.
+        bool first = spec && (ev0 >> qc & 1u) && ((uint32_t)(g0.sec >> (16 * qc)) & 63u) == lc;
+        if (first) ev0 &= ~(1u << qc);
+        uint32_t jq0 = jqc, ha = first ? a0 : 1u, hb = first ? b0 : 0u;  // a > b: nothing
+        for (;;) {
+            if (!__any(first || (ev0 | ev1) != 0)) break;
+            if (!first) {
+                ha = 1, hb = 0;
+                if (ev0) {
+                    const uint32_t q = (uint32_t)__builtin_ctz(ev0);
+                    ev0 &= ev0 - 1;
+                    jq0 = te0 * kTileKeys + q * kGroupKeys + 4 * ((uint32_t)(g0.sec >> (16 * q)) & 63u);
+                    ha = a0, hb = b0;
+                }
+                lq_load(base, jq0, ha, hb, x0);
+            }
+            uint32_t jq1 = 0, ta = 1, tb = 0;
+            if (ev1) {
+                const uint32_t q = (uint32_t)__builtin_ctz(ev1);
+                ev1 &= ev1 - 1;
+                jq1 = te1 * kTileKeys + q * kGroupKeys + 4 * ((uint32_t)(g1.sec >> (16 * q)) & 63u);
+                ta = a1, tb = b1;
+            }
+            lq_load(base, jq1, ta, tb, x1);
+            lq_eval(pf, tl, th, base, x0, jq0, ha, hb, bk, bj);
+            lq_eval(pf, tl, th, base, x1, jq1, ta, tb, bk, bj);
+            first = false;
+        }
+
+        // groups two lanes reach: exact scans by the whole wave, one lane's range at a time
+        // (from the first to the last such group of the range), a group per memory round trip
+#pragma unroll 1
+        for (int r = 0; r < 2; ++r) {
+            const uint32_t sv = r == 0 ? sc0 : sc1;
+            const uint32_t te = r == 0 ? te0 : te1, ra = r == 0 ? a0 : a1, rb = r == 0 ? b0 : b1;
+            uint32_t sa = 1, sb = 0;
+            if (sv) {
+                const uint32_t qlo = (uint32_t)__builtin_ctz(sv), qhi = 31u - (uint32_t)__builtin_clz(sv);
+                sa = max(ra, te * kTileKeys + qlo * kGroupKeys);
+                sb = min(rb, te * kTileKeys + (qhi + 1) * kGroupKeys - 1);
+            }
+            for (uint64_t m = __ballot(sa <= sb); m; m &= m - 1) {
+                const int l = __builtin_ctzll(m);
+                const uint32_t la = (uint32_t)__builtin_amdgcn_readlane(sa, l);
+                const uint32_t lb = (uint32_t)__builtin_amdgcn_readlane(sb, l);
+                const uint8_t *lbase = reinterpret_cast<const uint8_t *>(lane_u64((uint64_t)base, l));
+                uint64_t ek = 0, ej = ~0ull;
+                scan_range<kGroupKeys / 64>(tl, th, lbase, la, lb, ek, ej);
+                wave_best(ek, ej);
+                if (lane == (uint32_t)l && ek != 0) take_best32(ek, (uint32_t)ej, bk, bj);
+            }
+        }
+
+        // the step's cut(s): chain_step_small's decisions (adapters.cpp:48-69)
+        if (walking) {
+            int kind = kStepStop;
+            uint64_t c1 = 0, c2 = 0;
+            if (argmax) {
+                uint32_t idx = bk > 0 ? 4u * (bj - s4) : 0u;
+                if (idx < minl) idx = (minl + 3) & ~3u;  // adapters.cpp:66-67
+                if (idx != 0) {
+                    c1 = pos + idx;
+                    kind = kStepCut;
+                }
+            }
+            if (kind != kStepCut && !prm.open && !(argmax && rem >= 2ull * maxl)) {
+                uint64_t c;  // the tail rule (adapters.cpp:48-55); argmax with idx 0 is S7 UB
+                if (rem <= maxl) c = rem;
+                else if (rem < (uint64_t)maxl + minl) c = rem / 2;
+                else c = maxl;
+                if (c != 0) {
+                    c1 = pos + c;
+                    kind = kStepTail1;
+                    if (c < rem) {
+                        c2 = L;
+                        kind = kStepTail2;
+                    }
+                }
+            }
+            if (kind != kStepStop) {
+                if (n < cap) out[n++] = c1;
+                else overflow = true;
+                if (kind == kStepTail2) {
+                    if (n < cap) out[n++] = c2;
+                    else overflow = true;
+                }
+            }
+            if (kind != kStepCut || overflow) walking = false;
+            pos = c1;
+            if (pos >= L || n >= prm.max_steps) walking = false;
+        }
+    }
+    if (mine) counts[s] = overflow ? -1 : (int64_t)n;
 }
 
 // ---- parallel join of the speculative lists (multi-segment streams)
@@ -1789,7 +2129,7 @@ int rc_diag_read(uint64_t *out, uint32_t cap, uint32_t *n) {
 #endif
 
 int rc_launch_tiles(const KeyTables *d_tables, StreamDesc desc, uint64_t n_streams,
-                    uint64_t n_tiles, TileRecord *d_records, uint64_t *d_gmax,
+                    uint64_t n_tiles, TileRecord *d_records, GroupRecord *d_grp,
                     uint32_t *d_xlist, void *stream, void *mid_event) {
     hipStream_t st = (hipStream_t)stream;
     if (n_tiles == 0) {
@@ -1803,13 +2143,13 @@ int rc_launch_tiles(const KeyTables *d_tables, StreamDesc desc, uint64_t n_strea
     // the tie lists: n_tiles slots, then one count per wave
     uint32_t *d_xcount = d_xlist + n_tiles;
     const uint64_t n_waves = grid * waves_per_wg;
-    if (d_gmax)
+    if (d_grp)
         hipLaunchKernelGGL(rc_tile_kernel<kTileGroups>, dim3((unsigned)grid), dim3(1024), 0, st,
-                           d_tables, desc, n_streams, n_tiles, d_records, d_gmax, d_xlist,
+                           d_tables, desc, n_streams, n_tiles, d_records, d_grp, d_xlist,
                            d_xcount);
     else
         hipLaunchKernelGGL(rc_tile_kernel<1>, dim3((unsigned)grid), dim3(1024), 0, st, d_tables,
-                           desc, n_streams, n_tiles, d_records, d_gmax, d_xlist, d_xcount);
+                           desc, n_streams, n_tiles, d_records, d_grp, d_xlist, d_xcount);
     if (launch_status("rc_tile_kernel")) return 1;
     if (mid_event && hipEventRecord((hipEvent_t)mid_event, st) != hipSuccess) {
         snprintf(g_launch_err, sizeof g_launch_err, "hipEventRecord failed");
@@ -1820,7 +2160,7 @@ int rc_launch_tiles(const KeyTables *d_tables, StreamDesc desc, uint64_t n_strea
     if (egrid > 4 * cus) egrid = 4 * cus;
     if (egrid == 0) egrid = 1;
     hipLaunchKernelGGL(rc_edge_kernel, dim3((unsigned)egrid), dim3(256), 0, st, d_tables, desc,
-                       n_streams, n_tiles, d_records, d_gmax, (const uint32_t *)d_xlist,
+                       n_streams, n_tiles, d_records, d_grp, (const uint32_t *)d_xlist,
                        (const uint32_t *)d_xcount, n_waves);
     return launch_status("rc_edge_kernel");
 }
@@ -1831,6 +2171,18 @@ int rc_launch_chain(const KeyTables *d_tables, StreamDesc desc, uint64_t n_strea
                     uint64_t *d_seg_counts, bool any_multi, void *stream) {
     if (n_streams == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
+    // many single-segment streams with small windows and group bounds: one lane per stream
+    if (prm.lane && prm.lean && prm.grp && !any_multi && n_segs == n_streams &&
+        prm.max_steps != 0 && prm.window / kTileKeys <= (uint64_t)kLaneFull) {
+        const uint64_t grid = (n_streams + 255) / 256;
+        if (prm.window / kTileKeys <= 4)
+            hipLaunchKernelGGL(rc_lane_chain_kernel<4>, dim3((unsigned)grid), dim3(256), 0, st,
+                               d_tables, desc, n_streams, prm, d_records, d_cuts, d_counts);
+        else
+            hipLaunchKernelGGL(rc_lane_chain_kernel<kLaneFull>, dim3((unsigned)grid), dim3(256), 0,
+                               st, d_tables, desc, n_streams, prm, d_records, d_cuts, d_counts);
+        return launch_status("rc_lane_chain_kernel");
+    }
     // 4-wave workgroups on 20 KiB of LDS (compact tables)
     const bool small = prm.window / kTileKeys + 3 <= 64;  // window + both edge tiles in one row
     const uint64_t grid = (n_segs + kChainWaves - 1) / kChainWaves;
