@@ -149,12 +149,14 @@ uint64_t rc_host_key(const rc_chunker *ch, uint64_t d);
  * NULL): per quarter q, u16 at bits 16q = min(0xffff - B, 1023) << 6 | l, l the lowest of the
  * tile kernel's 64 lanes whose own maximum in the quarter equals the quarter's (lane l holds
  * keys 256 i + 4 l .. 256 i + 4 l + 3 of each of the quarter's iterations i) and B the top-16
- * maximum of the quarter's keys in every other lane; 0 where gmax is ~0.  *n_tiles receives the
- * tile count; at most cap are copied.  Blocking. */
+ * maximum of the quarter's keys in every other lane; 0 where gmax is ~0.  gthird (may be
+ * NULL): the same for the runner-up, min(0xffff - B3, 1023) << 6 | l1 with l1 the lowest lane
+ * other than l holding B, and B3 the maximum over every lane but l and l1.  *n_tiles receives
+ * the tile count; at most cap are copied.  Blocking. */
 int rc_tile_records(rc_chunker *ch, uint64_t n, const uint8_t *const *d_streams,
                     const uint64_t *lens, const uint64_t *last_piece, uint64_t *keys,
-                    uint64_t *js, uint64_t *gmax, uint64_t *gsec, uint64_t cap,
-                    uint64_t *n_tiles);
+                    uint64_t *js, uint64_t *gmax, uint64_t *gsec, uint64_t *gthird,
+                    uint64_t cap, uint64_t *n_tiles);
 uint64_t rc_tile_keys(void);
 
 /* Host-only check of the table construction (no device needed): out[i] = key of data word

@@ -815,8 +815,8 @@ uint64_t rc_tile_keys(void) { return kTileKeys; }
 
 int rc_tile_records(rc_chunker *ch, uint64_t n, const uint8_t *const *d_streams,
                     const uint64_t *lens, const uint64_t *last_piece, uint64_t *keys,
-                    uint64_t *js, uint64_t *gmax, uint64_t *gsec, uint64_t cap,
-                    uint64_t *n_tiles) {
+                    uint64_t *js, uint64_t *gmax, uint64_t *gsec, uint64_t *gthird,
+                    uint64_t cap, uint64_t *n_tiles) {
     if (!ch || !n_tiles) return fail(RC_ERR_ARGUMENT, "null argument");
     if (int rc = validate_streams(n, d_streams, lens, last_piece, true)) return rc;
     std::lock_guard<std::mutex> lock(ch->mu);
@@ -847,6 +847,7 @@ int rc_tile_records(rc_chunker *ch, uint64_t n, const uint8_t *const *d_streams,
         js[t] = h[t].j;
         if (gmax) gmax[t] = hg[t].max;
         if (gsec) gsec[t] = hg[t].sec;
+        if (gthird) gthird[t] = hg[t].third;
     }
     return RC_OK;
 }

@@ -27,6 +27,10 @@ constexpr int kChainWaves = 4;       // waves (= streams) per workgroup of the c
 #define RC_TILE_GROUPS 4
 #endif
 constexpr int kTileGroups = RC_TILE_GROUPS;  // key groups per tile with group maxima (<= 4: one u64)
+#ifndef RC_GROUP_THIRD
+#define RC_GROUP_THIRD 1
+#endif
+constexpr bool kGroupThird = RC_GROUP_THIRD != 0;  // group bounds carry the runner-up lane too
 constexpr int kGroupKeys = kTileKeys / kTileGroups;
 
 // ---- LDS image of the tile kernel -------------------------------------------------------
@@ -74,10 +78,14 @@ struct TileRecord {
 //        lane's keys of the group -- so every key of the group outside lane l has
 //        top16 <= 0xffff - (sec_g >> 6) = max(B, 0xfc00).  (Exact near the top, where the
 //        chain's thresholds lie: the maximum of ~1000 keys is within 1023 of 0xffff.)
-// A tile computed exactly (rc_edge_kernel) has max = ~0 and sec = 0: no bound at all.
+//   third: the same for the runner-up: u16 g = min(0xffff - B3, 1023) << 6 | l1, l1 the lowest
+//        lane other than l whose own maximum is B, B3 the maximum over every lane but l and l1.
+// A tile computed exactly (rc_edge_kernel) has max = ~0 and sec = third = 0: no bound at all.
 struct GroupRecord {
     uint64_t max;
     uint64_t sec;
+    uint64_t third;
+    uint64_t pad;  // 32 bytes: two 16-byte stores / loads
 };
 __host__ __device__ inline uint32_t group_sec_field(uint32_t B, uint32_t lane) {
     const uint32_t d = 0xffffu - B;

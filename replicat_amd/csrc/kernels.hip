@@ -466,21 +466,31 @@ __device__ __forceinline__ void stage_tile_tables(const KeyTables *tab) {
 template <int G>
 __device__ __forceinline__ GroupRecord tile_groups(const uint32_t (&gpk)[(G + 1) / 2]) {
     const uint32_t lane = lane_id();
-    uint64_t gm = 0, gs = 0;
+    uint64_t gm = 0, gs = 0, g3 = 0;
+    // lowest lane whose packed half equals m's (every lane is live in the tile kernel, and m is
+    // always some remaining lane's value)
+    auto arg = [&](uint32_t v, uint32_t m, bool hi) {
+        return (uint32_t)__builtin_ctzll(__ballot(hi ? (v >> 16) == (m >> 16) : (v & 0xffffu) == (m & 0xffffu)));
+    };
+    auto drop = [&](uint32_t la, uint32_t lb) {  // clears lane la's low half and lane lb's high half
+        return (lane == la ? 0u : 0xffffu) | (lane == lb ? 0u : 0xffff0000u);
+    };
 #pragma unroll
     for (int i = 0; i < (G + 1) / 2; ++i) {
         const uint32_t v = gpk[i];
         const uint32_t mx = wave_max_pk16(v);
-        // every lane is live in the tile kernel, so each maximum is some lane's
-        const uint32_t l0 = (uint32_t)__builtin_ctzll(__ballot((v & 0xffffu) == (mx & 0xffffu)));
-        const uint32_t l1 = (uint32_t)__builtin_ctzll(__ballot((v >> 16) == (mx >> 16)));
-        const uint32_t keep = (lane == l0 ? 0u : 0xffffu) | (lane == l1 ? 0u : 0xffff0000u);
-        const uint32_t sec = wave_max_pk16(v & keep);
+        const uint32_t a0 = arg(v, mx, false), b0 = arg(v, mx, true);
+        const uint32_t v1 = v & drop(a0, b0);
+        const uint32_t sec = wave_max_pk16(v1);
         gm |= (uint64_t)mx << (32 * i);
-        const uint32_t f = group_sec_field(sec & 0xffffu, l0) | group_sec_field(sec >> 16, l1) << 16;
-        gs |= (uint64_t)f << (32 * i);
+        gs |= (uint64_t)(group_sec_field(sec & 0xffffu, a0) | group_sec_field(sec >> 16, b0) << 16) << (32 * i);
+        if constexpr (kGroupThird) {
+            const uint32_t a1 = arg(v1, sec, false), b1 = arg(v1, sec, true);
+            const uint32_t thr = wave_max_pk16(v1 & drop(a1, b1));
+            g3 |= (uint64_t)(group_sec_field(thr & 0xffffu, a1) | group_sec_field(thr >> 16, b1) << 16) << (32 * i);
+        }
     }
-    return GroupRecord{gm, gs};
+    return GroupRecord{gm, gs, g3, 0};
 }
 
 // Persistent: one 1024-thread workgroup per CU, each wave a contiguous range of tiles.
@@ -651,7 +661,7 @@ __device__ __forceinline__ void exact_tile(const uint64_t *tl, const uint64_t *t
     if (lane_id() == 0) {
         rec[t].key = bk;
         rec[t].j = bj;
-        if (grp) grp[t] = GroupRecord{~0ull, 0ull};  // no group bounds for an exact tile
+        if (grp) grp[t] = GroupRecord{~0ull, 0ull, 0ull, 0ull};  // no group bounds: exact tile
     }
 }
 
@@ -928,9 +938,18 @@ __device__ uint32_t g_diag_n;
             g_diag[g_diag_n++] = ((uint64_t)(tag) << 56) | __builtin_amdgcn_s_memrealtime(); \
         }                                                                              \
     } while (0)
+#define RC_LSTAMP(tag)                                                                 \
+    do {                                                                               \
+        if (diag && lane_id() == 0 && g_diag_n < 4000) {                               \
+            g_diag[g_diag_n++] = ((uint64_t)(tag) << 56) | __builtin_amdgcn_s_memrealtime(); \
+        }                                                                              \
+    } while (0)
 #else
 #define RC_STAMP(tag) \
     do {              \
+    } while (0)
+#define RC_LSTAMP(tag) \
+    do {               \
     } while (0)
 #endif
 
@@ -1431,22 +1450,31 @@ __global__ __launch_bounds__(kChainWaves * 64) void rc_spec_kernel(const KeyTabl
 constexpr int kLaneFull = 8;  // widest window of the lane chain: window keys / kTileKeys <= 8
 constexpr int kLaneIters = kTileIters / kTileGroups;  // tile-kernel iterations per group
 
-// Group classification of one edge range [a, b] inside tile te: bits of the groups whose lane-l0
-// keys are to be evaluated (ev) and of the groups left to an exact scan (sc).
-__device__ __forceinline__ void lane_groups(bool live, const GroupRecord &g, uint32_t te,
-                                            uint32_t a, uint32_t b, uint32_t t16, uint32_t &ev,
-                                            uint32_t &sc) {
-    ev = sc = 0;
-    if (!live) return;
+// Group classification of one edge range [a, b] inside tile te, as task bits: bit q = evaluate
+// group q's lane l0, bit kTileGroups + q = its lane l1 too; sc = the groups left to an exact
+// scan (three lanes reach the best).
+__device__ __forceinline__ uint32_t lane_groups(bool live, const GroupRecord &g, uint32_t te,
+                                                uint32_t a, uint32_t b, uint32_t t16,
+                                                uint32_t &sc) {
+    uint32_t ev = 0;
+    sc = 0;
+    if (!live) return 0;
     const uint32_t tj0 = te * kTileKeys;
     const uint32_t qa = (a - tj0) / kGroupKeys, qb = (b - tj0) / kGroupKeys;
 #pragma unroll
     for (uint32_t q = 0; q < (uint32_t)kTileGroups; ++q) {
         if (q < qa || q > qb) continue;
         if (((uint32_t)(g.max >> (16 * q)) & 0xffffu) < t16) continue;  // nothing reaches the best
-        if (group_sec_bound((uint32_t)(g.sec >> (16 * q)) & 0xffffu) < t16) ev |= 1u << q;  // l0 only
-        else sc |= 1u << q;
+        ev |= 1u << q;                                                     // lane l0
+        if (group_sec_bound((uint32_t)(g.sec >> (16 * q)) & 0xffffu) < t16) continue;
+        if (!kGroupThird) {
+            sc |= 1u << q;
+            continue;
+        }
+        ev |= 1u << (kTileGroups + q);                                     // lane l1 as well
+        if (group_sec_bound((uint32_t)(g.third >> (16 * q)) & 0xffffu) >= t16) sc |= 1u << q;
     }
+    return ev;
 }
 
 // top-16 of key j from the prefilter entries of its two words (gclmul.h)
@@ -1455,7 +1483,7 @@ __device__ __forceinline__ uint32_t top16_of(uint32_t e_lo_word, uint32_t e_hi_w
 }
 
 // One lane's keys in one group: keys jq + 256 i .. jq + 256 i + 3 (i < kLaneIters), jq =
-// the group's first key + 4 l -- one 16-byte block and the word before it per iteration.
+// the group's first key + 4 l -- one 16-byte block per iteration and the word before it.
 struct LaneQuarter {
     uint32_t w[kLaneIters][5];  // the word before each block, then the block's 4 words
 };
@@ -1481,23 +1509,25 @@ __device__ __forceinline__ void lq_load(const uint8_t *base, uint32_t jq, uint32
     }
 }
 
-// Folds the keys of x in [a, b] into (bk, bj): top-16 values from the compact prefilter, then
-// the exact key of the one with the largest top-16 value that reaches bk's -- a key with a
-// smaller top-16 value is smaller -- or, when two share it (rare), of every key exactly.
-__device__ __forceinline__ void lq_eval(const uint32_t *pf, const uint64_t *tl, const uint64_t *th,
-                                        const uint8_t *base, const LaneQuarter &x, uint32_t jq,
-                                        uint32_t a, uint32_t b, uint64_t &bk, uint32_t &bj) {
-    const uint32_t t16 = (uint32_t)(bk >> 48);
+// The candidate among the keys of x in [a, b]: the one with the largest top-16 value (from the
+// prefilter) that reaches t16 -- a key with a smaller top-16 value is smaller -- and whether
+// another key shares that value (then every key of the lane is evaluated exactly: rare).
+struct LaneCand {
+    bool have, tie;
+    uint32_t ct, cj;
+};
+
+__device__ __forceinline__ LaneCand lq_scan(const uint32_t *pf, const LaneQuarter &x, uint32_t jq,
+                                            uint32_t a, uint32_t b, uint32_t t16) {
     bool have = false, tie = false;
-    uint32_t ct = 0, cj = 0, clo = 0, chi = 0;
+    uint32_t ct = 0, cj = 0;
 #pragma unroll
     for (int i = 0; i < kLaneIters; ++i) {
         const uint32_t j4 = jq + 256 * i;
         if (!(j4 <= b && j4 + 3 >= a)) continue;
-        const uint32_t *wd = x.w[i];
         uint32_t e[5];
 #pragma unroll
-        for (int k = 0; k < 5; ++k) e[k] = pfc_entry(pf, wd[k]);
+        for (int k = 0; k < 5; ++k) e[k] = pfc_entry(pf, x.w[i][k]);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint32_t j = j4 + k, t = top16_of(e[k], e[k + 1]);
@@ -1507,23 +1537,74 @@ __device__ __forceinline__ void lq_eval(const uint32_t *pf, const uint64_t *tl, 
                     tie = false;
                     ct = t;
                     cj = j;
-                    clo = wd[k];
-                    chi = wd[k + 1];
                 } else if (t == ct) {
                     tie = true;
                 }
             }
         }
     }
-    if (have) take_best32(full_key(tl, th, clo, chi), cj, bk, bj);
-    if (tie) {  // every key of the lane in range, its words read again (rolled: rare, small code)
+    return LaneCand{have, tie, ct, cj};
+}
+
+// Every key of lane jq's blocks in [a, b] exactly, its words read again (rolled: rare, small code)
+__device__ __forceinline__ void lq_all(const uint64_t *tl, const uint64_t *th, const uint8_t *base,
+                                       uint32_t jq, uint32_t a, uint32_t b, uint64_t &bk,
+                                       uint32_t &bj) {
 #pragma unroll 1
-        for (uint32_t i = 0; i < 4 * kLaneIters; ++i) {
-            const uint32_t j = jq + 256 * (i >> 2) + (i & 3);
-            if (j >= a && j <= b)
-                take_best32(full_key(tl, th, ld_u32(base + 4ull * j - 4), ld_u32(base + 4ull * j)), j, bk, bj);
-        }
+    for (uint32_t i = 0; i < 4 * kLaneIters; ++i) {
+        const uint32_t j = jq + 256 * (i >> 2) + (i & 3);
+        if (j >= a && j <= b)
+            take_best32(full_key(tl, th, ld_u32(base + 4ull * j - 4), ld_u32(base + 4ull * j)), j, bk, bj);
     }
+}
+
+// Two lanes' candidates folded into (bk, bj): their words read again (cache hits, both in
+// flight together) -- cheaper than carrying each candidate's words through the scan.
+__device__ __forceinline__ void lq_fold(const uint64_t *tl, const uint64_t *th, const uint8_t *base,
+                                        const LaneCand &c0, uint32_t jq0, uint32_t a0, uint32_t b0,
+                                        const LaneCand &c1, uint32_t jq1, uint32_t a1, uint32_t b1,
+                                        uint64_t &bk, uint32_t &bj) {
+    uint32_t w00 = 0, w01 = 0, w10 = 0, w11 = 0;
+    if (c0.have) {
+        w00 = ld_u32(base + 4ull * c0.cj - 4);
+        w01 = ld_u32(base + 4ull * c0.cj);
+    }
+    if (c1.have) {
+        w10 = ld_u32(base + 4ull * c1.cj - 4);
+        w11 = ld_u32(base + 4ull * c1.cj);
+    }
+    if (c0.have) take_best32(full_key(tl, th, w00, w01), c0.cj, bk, bj);
+    if (c1.have) take_best32(full_key(tl, th, w10, w11), c1.cj, bk, bj);
+    if (c0.tie) lq_all(tl, th, base, jq0, a0, b0, bk, bj);
+    if (c1.tie) lq_all(tl, th, base, jq1, a1, b1, bk, bj);
+}
+
+// The 6-bit lanes of a GroupRecord lane word's kTileGroups fields, one per byte.
+__device__ __forceinline__ uint32_t lane_bytes(uint64_t f) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int q = 0; q < kTileGroups; ++q) r |= (uint32_t)((f >> (16 * q)) & 63u) << (8 * q);
+    return r;
+}
+
+// Pops the next of a lane's tasks (lane_groups bits: head l0 / l1 groups, then the tail's) as the
+// first key block jq of the task's lane and the range [a, b]; a > b when there is none.  hl / tl:
+// lane_bytes of the head / tail tile's sec (low half) and third (high half).  Plain values
+// throughout: a conditional between references would be a select of addresses, which LLVM
+// keeps in scratch memory.
+__device__ __forceinline__ void pop_task(uint32_t &tasks, uint64_t hl, uint64_t tl, uint32_t te0,
+                                         uint32_t te1, uint32_t a0, uint32_t b0, uint32_t a1,
+                                         uint32_t b1, uint32_t &jq, uint32_t &a, uint32_t &b) {
+    a = 1, b = 0;
+    if (!tasks) return;
+    const uint32_t bit = (uint32_t)__builtin_ctz(tasks);
+    tasks &= tasks - 1;
+    const bool tail = bit >= 2 * kTileGroups;
+    const uint32_t q = bit % kTileGroups, sh = (bit / kTileGroups & 1u) * 32 + 8 * q;
+    const uint32_t lane = (uint32_t)((tail ? tl : hl) >> sh) & 63u;
+    jq = (tail ? te1 : te0) * kTileKeys + q * kGroupKeys + 4 * lane;
+    a = tail ? a1 : a0;
+    b = tail ? b1 : b0;
 }
 
 // Best exact key over [a, b] of one stream by the whole wave, 64 * U keys per memory round trip.
@@ -1579,8 +1660,12 @@ __global__ __launch_bounds__(256) void rc_lane_chain_kernel(const KeyTables *__r
 
     uint64_t pos = 0, n = 0;
     bool walking = mine && L > 0 && prm.max_steps > 0, overflow = false;
+#ifdef RC_DIAG_STAMPS
+    const bool diag = gid < 64;  // wave 0: per-phase stamps (diagnostic build only)
+#endif
     for (;;) {
         if (!__any(walking)) break;
+        RC_LSTAMP(1);
         const uint64_t rem = L - pos;
         const bool argmax = (P >= pos && P - pos >= maxl) || rem >= 2ull * maxl;
         const uint32_t s4 = (uint32_t)(pos >> 2);
@@ -1624,48 +1709,48 @@ __global__ __launch_bounds__(256) void rc_lane_chain_kernel(const KeyTables *__r
             if (inr) take_best32(r1.key, rj, bk, bj);
             if (r1.key == 0 || inr || r1.key <= bk) live1 = false;
         }
-        uint32_t ev0, sc0, ev1, sc1;
-        lane_groups(live0, g0, te0, a0, b0, (uint32_t)(bk >> 48), ev0, sc0);
-        lane_groups(live1, g1, te1, a1, b1, (uint32_t)(bk >> 48), ev1, sc1);
+        uint32_t sc0, sc1;
+        RC_LSTAMP(2);
+        // tasks: bits 0..2G-1 the head's (lane l0 of group q, then lane l1), 2G.. the tail's
+        uint32_t tasks = lane_groups(live0, g0, te0, a0, b0, (uint32_t)(bk >> 48), sc0);
+        tasks |= lane_groups(live1, g1, te1, a1, b1, (uint32_t)(bk >> 48), sc1) << (2 * kTileGroups);
+        // the tasks' lanes, one byte per group: head l0 / l1, tail l0 / l1
+        const uint64_t hl = (uint64_t)lane_bytes(g0.third) << 32 | lane_bytes(g0.sec);
+        const uint64_t tll = (uint64_t)lane_bytes(g1.third) << 32 | lane_bytes(g1.sec);
+        auto task = [&](uint32_t &jq, uint32_t &a, uint32_t &b) {
+            pop_task(tasks, hl, tll, te0, te1, a0, b0, a1, b1, jq, a, b);
+        };
 
-        // groups handed to their lane l0, one of the head's and one of the tail's per round, the
-        // loads of both in flight together.  The head's first is, as a rule, the previous cut's
-        // own group and lane (that cut's key is the maximum of the previous window): its words
-        // came with the records.
-        bool first = spec && (ev0 >> qc & 1u) && ((uint32_t)(g0.sec >> (16 * qc)) & 63u) == lc;
-        if (first) ev0 &= ~(1u << qc);
-        uint32_t jq0 = jqc, ha = first ? a0 : 1u, hb = first ? b0 : 0u;  // a > b: nothing
+        // the lanes' keys, two tasks per round with their loads in flight together.  The
+        // first is, as a rule, the previous cut's own group and lane (that cut's key is the
+        // maximum of the previous window): its words came with the records.
+        bool first = spec && (tasks >> qc & 1u) && ((uint32_t)(hl >> (8 * qc)) & 63u) == lc;
+        if (first) tasks &= ~(1u << qc);
+        uint32_t jq0 = jqc, ha = first ? a0 : 1u, hb = first ? b0 : 0u;
         for (;;) {
-            if (!__any(first || (ev0 | ev1) != 0)) break;
+            if (!__any(first || tasks != 0)) break;
             if (!first) {
-                ha = 1, hb = 0;
-                if (ev0) {
-                    const uint32_t q = (uint32_t)__builtin_ctz(ev0);
-                    ev0 &= ev0 - 1;
-                    jq0 = te0 * kTileKeys + q * kGroupKeys + 4 * ((uint32_t)(g0.sec >> (16 * q)) & 63u);
-                    ha = a0, hb = b0;
-                }
+                task(jq0, ha, hb);
                 lq_load(base, jq0, ha, hb, x0);
             }
-            uint32_t jq1 = 0, ta = 1, tb = 0;
-            if (ev1) {
-                const uint32_t q = (uint32_t)__builtin_ctz(ev1);
-                ev1 &= ev1 - 1;
-                jq1 = te1 * kTileKeys + q * kGroupKeys + 4 * ((uint32_t)(g1.sec >> (16 * q)) & 63u);
-                ta = a1, tb = b1;
-            }
+            uint32_t jq1 = 0, ta, tb;
+            task(jq1, ta, tb);
             lq_load(base, jq1, ta, tb, x1);
-            lq_eval(pf, tl, th, base, x0, jq0, ha, hb, bk, bj);
-            lq_eval(pf, tl, th, base, x1, jq1, ta, tb, bk, bj);
+            const uint32_t t16 = (uint32_t)(bk >> 48);
+            const LaneCand c0 = lq_scan(pf, x0, jq0, ha, hb, t16);
+            const LaneCand c1 = lq_scan(pf, x1, jq1, ta, tb, t16);
+            lq_fold(tl, th, base, c0, jq0, ha, hb, c1, jq1, ta, tb, bk, bj);
             first = false;
+            RC_LSTAMP(3);
         }
+        RC_LSTAMP(4);
 
-        // groups two lanes reach: exact scans by the whole wave, one lane's range at a time
+        // groups three lanes reach: exact scans by the whole wave, one lane's range at a time
         // (from the first to the last such group of the range), a group per memory round trip
 #pragma unroll 1
         for (int r = 0; r < 2; ++r) {
-            const uint32_t sv = r == 0 ? sc0 : sc1;
-            const uint32_t te = r == 0 ? te0 : te1, ra = r == 0 ? a0 : a1, rb = r == 0 ? b0 : b1;
+            const uint32_t sv = r == 0 ? +sc0 : +sc1;  // values, not a select of addresses
+            const uint32_t te = r == 0 ? +te0 : +te1, ra = r == 0 ? +a0 : +a1, rb = r == 0 ? +b0 : +b1;
             uint32_t sa = 1, sb = 0;
             if (sv) {
                 const uint32_t qlo = (uint32_t)__builtin_ctz(sv), qhi = 31u - (uint32_t)__builtin_clz(sv);
@@ -1681,8 +1766,10 @@ __global__ __launch_bounds__(256) void rc_lane_chain_kernel(const KeyTables *__r
                 scan_range<kGroupKeys / 64>(tl, th, lbase, la, lb, ek, ej);
                 wave_best(ek, ej);
                 if (lane == (uint32_t)l && ek != 0) take_best32(ek, (uint32_t)ej, bk, bj);
+                RC_LSTAMP(5);
             }
         }
+        RC_LSTAMP(6);
 
         // the step's cut(s): chain_step_small's decisions (adapters.cpp:48-69)
         if (walking) {
