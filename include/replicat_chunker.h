@@ -145,18 +145,18 @@ uint64_t rc_host_key(const rc_chunker *ch, uint64_t d);
  * the stream.  A tile's keys are all of j0 .. j0 + rc_tile_keys() - 1 when their bytes lie in
  * the stream, else those up to jneed; key 0 never counts.  gmax (may be NULL): for chunkers
  * with small windows (max_length below ~1 MB) the top-16 maximum of each quarter of the tile
- * (u16 q at bits 16q), ~0 for a tile computed exactly or a chunker without them.  gsec (may be
- * NULL): per quarter q, u16 at bits 16q = min(0xffff - B, 1023) << 6 | l, l the lowest of the
- * tile kernel's 64 lanes whose own maximum in the quarter equals the quarter's (lane l holds
- * keys 256 i + 4 l .. 256 i + 4 l + 3 of each of the quarter's iterations i) and B the top-16
- * maximum of the quarter's keys in every other lane; 0 where gmax is ~0.  gthird (may be
- * NULL): the same for the runner-up, min(0xffff - B3, 1023) << 6 | l1 with l1 the lowest lane
- * other than l holding B, and B3 the maximum over every lane but l and l1.  *n_tiles receives
- * the tile count; at most cap are copied.  Blocking. */
+ * (u16 q at bits 16q), ~0 for a tile computed exactly or a chunker without them.  ghot (may be
+ * NULL, 4 words per tile): ghot[4t + q] bit l = lane l of the tile kernel (which holds keys
+ * 256 i + 4 l .. 256 i + 4 l + 3 of each of the quarter's iterations i) has a key in quarter q
+ * whose top 16 bits reach rc_group_hot_threshold(ch); all ones where gmax is ~0.  *n_tiles
+ * receives the tile count; at most cap are copied.  Blocking. */
 int rc_tile_records(rc_chunker *ch, uint64_t n, const uint8_t *const *d_streams,
                     const uint64_t *lens, const uint64_t *last_piece, uint64_t *keys,
-                    uint64_t *js, uint64_t *gmax, uint64_t *gsec, uint64_t *gthird,
-                    uint64_t cap, uint64_t *n_tiles);
+                    uint64_t *js, uint64_t *gmax, uint64_t *ghot, uint64_t cap,
+                    uint64_t *n_tiles);
+/* The top-16 value from which a lane of a tile quarter counts as hot in rc_tile_records (a
+ * function of max_length: 10 / window of the 16-bit range below the top; 0 = none). */
+uint32_t rc_group_hot_threshold(const rc_chunker *ch);
 uint64_t rc_tile_keys(void);
 
 /* Host-only check of the table construction (no device needed): out[i] = key of data word

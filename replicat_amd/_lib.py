@@ -57,7 +57,8 @@ SIGNATURES = {
     'rc_keys_needed': (_u64, [_u64, _u64, _u64]),
     'rc_host_key': (_u64, [_p, _u64]),
     'rc_tables_key': (_int, [_p, _u64, _p, _p, _p]),
-    'rc_tile_records': (_int, [_p, _u64, _p, _p, _p, _p, _p, _p, _p, _p, _u64, ctypes.POINTER(_u64)]),
+    'rc_tile_records': (_int, [_p, _u64, _p, _p, _p, _p, _p, _p, _p, _u64, ctypes.POINTER(_u64)]),
+    'rc_group_hot_threshold': (_u32, [_p]),
     'rc_tile_keys': (_u64, []),
     # replicat_digest.h
     'rc_blake2b_create': (_int, [_u32, _int, ctypes.POINTER(_p)]),

@@ -109,25 +109,24 @@ class GpuChunker:
 
     def tile_records(self, ptrs, lens, last_piece=None, groups=False):
         """(keys, js) of the per-tile phase over device streams (inspection / tests); with
-        groups=True also the per-quarter group bounds (keys, js, gmax, gsec, gthird): see
-        rc_tile_records in include/replicat_chunker.h."""
+        groups=True also the per-quarter group bounds (keys, js, gmax, ghot, hot threshold):
+        see rc_tile_records in include/replicat_chunker.h."""
         ptrs, lens = _ptr_array(ptrs), _ptr_array(lens)
         last = _ptr_array(last_piece if last_piece is not None else np.zeros(len(lens)))
         nt = ctypes.c_uint64()
         check(lib().rc_tile_records(self._h, len(lens), ptrs.ctypes.data, lens.ctypes.data,
-                                    last.ctypes.data, None, None, None, None, None, 0,
+                                    last.ctypes.data, None, None, None, None, 0,
                                     ctypes.byref(nt)))
         keys = np.zeros(max(nt.value, 1), dtype=np.uint64)
         js = np.zeros(max(nt.value, 1), dtype=np.uint64)
         gm = np.zeros(max(nt.value, 1), dtype=np.uint64)
-        gs = np.zeros(max(nt.value, 1), dtype=np.uint64)
-        g3 = np.zeros(max(nt.value, 1), dtype=np.uint64)
+        gh = np.zeros((max(nt.value, 1), 4), dtype=np.uint64)
         check(lib().rc_tile_records(self._h, len(lens), ptrs.ctypes.data, lens.ctypes.data,
                                     last.ctypes.data, keys.ctypes.data, js.ctypes.data,
-                                    gm.ctypes.data, gs.ctypes.data, g3.ctypes.data, nt.value,
-                                    ctypes.byref(nt)))
+                                    gm.ctypes.data, gh.ctypes.data, nt.value, ctypes.byref(nt)))
         if groups:
-            return keys[:nt.value], js[:nt.value], gm[:nt.value], gs[:nt.value], g3[:nt.value]
+            return (keys[:nt.value], js[:nt.value], gm[:nt.value], gh[:nt.value],
+                    int(lib().rc_group_hot_threshold(self._h)))
         return keys[:nt.value], js[:nt.value]
 
     # ---------------------------------------------------------------------- profiling

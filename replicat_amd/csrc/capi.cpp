@@ -423,8 +423,9 @@ int upload_and_launch(rc_chunker *ch, Workspace &ws, const Plan &plan, ChainPara
     }
     // 32-bit chain steps: small windows (the one-row record cache) and key indices < 2^32
     prm.lean = ch->small && plan.max_len < (16ull << 30) ? 1u : 0u;
+    prm.hot = group_hot_threshold(ch->window);
     if (rc_launch_tiles(ch->d_tables, d, plan.n, plan.n_tiles,
-                        static_cast<TileRecord *>(ws.d_records.p), grp, tie_lists(ws, plan),
+                        static_cast<TileRecord *>(ws.d_records.p), grp, prm.hot, tie_lists(ws, plan),
                         stream, ch->timing ? ev[1] : nullptr))
         return fail(RC_ERR_HIP, "%s", rc_launch_error());
     if (ch->timing) HIP_TRY(hipEventRecord(ev[2], stream));
@@ -457,6 +458,7 @@ ChainParams chain_params(const rc_chunker *ch, const Plan &plan, uint64_t max_st
     p.n_tiles = 0;
     p.lean = 0;
     p.lane = 0;
+    p.hot = 0;
     return p;
 }
 
@@ -475,6 +477,8 @@ static const char kBuildId[] = "RC_BUILD_ID:" RC_BUILD_ID;
 const char *rc_build_id(void) { return kBuildId + 12; }
 
 const char *rc_last_error(void) { return g_err; }
+
+uint32_t rc_group_hot_threshold(const rc_chunker *ch) { return ch ? group_hot_threshold(ch->window) : 0u; }
 
 uint64_t rc_keys_needed(uint64_t max_length, uint64_t L, uint64_t P) {
     // S4: at chunk start s an argmax happens iff P - s >= max or L - s >= 2*max; the window of
@@ -815,8 +819,8 @@ uint64_t rc_tile_keys(void) { return kTileKeys; }
 
 int rc_tile_records(rc_chunker *ch, uint64_t n, const uint8_t *const *d_streams,
                     const uint64_t *lens, const uint64_t *last_piece, uint64_t *keys,
-                    uint64_t *js, uint64_t *gmax, uint64_t *gsec, uint64_t *gthird,
-                    uint64_t cap, uint64_t *n_tiles) {
+                    uint64_t *js, uint64_t *gmax, uint64_t *ghot, uint64_t cap,
+                    uint64_t *n_tiles) {
     if (!ch || !n_tiles) return fail(RC_ERR_ARGUMENT, "null argument");
     if (int rc = validate_streams(n, d_streams, lens, last_piece, true)) return rc;
     std::lock_guard<std::mutex> lock(ch->mu);
@@ -829,12 +833,13 @@ int rc_tile_records(rc_chunker *ch, uint64_t n, const uint8_t *const *d_streams,
     HIP_TRY(hipMemcpy(ws.d_desc.p, ws.h_desc.p, plan.bytes, hipMemcpyHostToDevice));
     GroupRecord *d_grp = ch->groups ? group_records(ws, plan) : nullptr;
     if (rc_launch_tiles(ch->d_tables, desc_view(ws.d_desc.p, n), n, plan.n_tiles,
-                        static_cast<TileRecord *>(ws.d_records.p), d_grp, tie_lists(ws, plan),
+                        static_cast<TileRecord *>(ws.d_records.p), d_grp,
+                        group_hot_threshold(ch->window), tie_lists(ws, plan),
                         nullptr, nullptr))
         return fail(RC_ERR_HIP, "%s", rc_launch_error());
     HIP_TRY(hipDeviceSynchronize());
     std::vector<TileRecord> h(plan.n_tiles);
-    std::vector<GroupRecord> hg(plan.n_tiles, GroupRecord{~0ull, 0ull});
+    std::vector<GroupRecord> hg(plan.n_tiles, GroupRecord{~0ull, {~0ull, ~0ull, ~0ull, ~0ull}, 0ull});
     if (plan.n_tiles) {
         HIP_TRY(hipMemcpy(h.data(), ws.d_records.p, plan.n_tiles * sizeof(TileRecord),
                           hipMemcpyDeviceToHost));
@@ -846,8 +851,8 @@ int rc_tile_records(rc_chunker *ch, uint64_t n, const uint8_t *const *d_streams,
         keys[t] = h[t].key;
         js[t] = h[t].j;
         if (gmax) gmax[t] = hg[t].max;
-        if (gsec) gsec[t] = hg[t].sec;
-        if (gthird) gthird[t] = hg[t].third;
+        if (ghot)
+            for (int g = 0; g < kTileGroups; ++g) ghot[kTileGroups * t + g] = hg[t].hot[g];
     }
     return RC_OK;
 }

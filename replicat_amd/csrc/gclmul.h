@@ -27,10 +27,6 @@ constexpr int kChainWaves = 4;       // waves (= streams) per workgroup of the c
 #define RC_TILE_GROUPS 4
 #endif
 constexpr int kTileGroups = RC_TILE_GROUPS;  // key groups per tile with group maxima (<= 4: one u64)
-#ifndef RC_GROUP_THIRD
-#define RC_GROUP_THIRD 1
-#endif
-constexpr bool kGroupThird = RC_GROUP_THIRD != 0;  // group bounds carry the runner-up lane too
 constexpr int kGroupKeys = kTileKeys / kTileGroups;
 
 // ---- LDS image of the tile kernel -------------------------------------------------------
@@ -72,26 +68,30 @@ struct TileRecord {
 // Per-tile group bounds of the small-window tile kernel (kTileGroups groups of kGroupKeys keys;
 // group g = the tile kernel's iterations g*kTileIters/G .., in which lane l holds keys
 // 256*it + 4l .. 256*it + 4l + 3):
-//   max: u16 g = the top-16 maximum of group g (keys that do not exist count as 0);
-//   sec: u16 g = min(0xffff - B, 1023) << 6 | l, with l the lowest lane whose own top-16
-//        maximum in the group equals the group's, and B the top-16 maximum over every OTHER
-//        lane's keys of the group -- so every key of the group outside lane l has
-//        top16 <= 0xffff - (sec_g >> 6) = max(B, 0xfc00).  (Exact near the top, where the
-//        chain's thresholds lie: the maximum of ~1000 keys is within 1023 of 0xffff.)
-//   third: the same for the runner-up: u16 g = min(0xffff - B3, 1023) << 6 | l1, l1 the lowest
-//        lane other than l whose own maximum is B, B3 the maximum over every lane but l and l1.
-// A tile computed exactly (rc_edge_kernel) has max = ~0 and sec = third = 0: no bound at all.
+//   max:     u16 g = the top-16 maximum of group g (keys that do not exist count as 0);
+//   hot[g]:  bit l = lane l's own top-16 maximum in group g is >= the chunker's hot threshold
+//            (group_hot_threshold: low enough that a window's best almost always reaches it,
+//            high enough that a group rarely has more than one such lane).
+// So when the best so far reaches the threshold, only the lanes in hot[g] can hold a key of the
+// group that reaches it.  A tile computed exactly (rc_edge_kernel) has max = ~0 and every lane
+// hot: no bound at all.
 struct GroupRecord {
     uint64_t max;
-    uint64_t sec;
-    uint64_t third;
-    uint64_t pad;  // 32 bytes: two 16-byte stores / loads
+    uint64_t hot[kTileGroups];
+    uint64_t pad;  // 48 bytes: three 16-byte stores / loads
 };
-__host__ __device__ inline uint32_t group_sec_field(uint32_t B, uint32_t lane) {
-    const uint32_t d = 0xffffu - B;
-    return (d < 1023u ? d : 1023u) << 6 | lane;
+static_assert(kTileGroups % 2 == 0 && sizeof(GroupRecord) % 16 == 0, "group record layout");
+
+// Hot threshold of a chunker whose argmax window holds `window` keys: 10 / window of the
+// 16-bit range below the top.  The best of the window's full tiles (>= 0.6 window keys) falls
+// below it with probability ~e^-6 or less, and a group of kGroupKeys keys has ~10 kGroupKeys /
+// window hot lanes besides its maximum's (0.5 for config 3 iii's 20,000-key windows).  0 for
+// windows of under a tile (nothing is excluded: the chain scans).
+__host__ __device__ inline uint32_t group_hot_threshold(uint64_t window) {
+    if (window < (uint64_t)kTileKeys) return 0;
+    const uint64_t below = (10 * 65536 + window - 1) / window;
+    return below >= 65536 ? 0u : (uint32_t)(65536 - below);
 }
-__host__ __device__ inline uint32_t group_sec_bound(uint32_t field) { return 0xffffu - (field >> 6); }
 
 struct ChainParams {
     uint64_t min_length;
@@ -107,6 +107,7 @@ struct ChainParams {
     uint32_t open;        // RC_OPEN: non-final prefix, no tail rule
     uint32_t lean;        // small windows and every stream < 16 GiB: 32-bit chain steps
     uint32_t lane;        // lane-per-stream chain allowed (rc_lane_chain_kernel; 2 = forced)
+    uint32_t hot;         // the group records' hot threshold (group_hot_threshold)
 };
 
 // splitmix64 finaliser (replicat_amd/synth.py)
@@ -129,7 +130,7 @@ extern "C" {
 // tile kernel's per-wave tie lists.
 int rc_launch_tiles(const rc::KeyTables *d_tables, rc::StreamDesc desc, uint64_t n_streams,
                     uint64_t n_tiles, rc::TileRecord *d_records, rc::GroupRecord *d_grp,
-                    uint32_t *d_xlist, void *stream, void *mid_event);
+                    uint32_t hot, uint32_t *d_xlist, void *stream, void *mid_event);
 int rc_launch_chain(const rc::KeyTables *d_tables, rc::StreamDesc desc, uint64_t n_streams,
                     rc::ChainParams prm, uint64_t n_segs, const rc::TileRecord *d_records,
                     uint64_t *d_cuts, int64_t *d_counts, uint64_t *d_scratch,

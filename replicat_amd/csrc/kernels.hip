@@ -460,37 +460,21 @@ __device__ __forceinline__ void stage_tile_tables(const KeyTables *tab) {
 }
 
 // Group bounds of one tile from the lanes' packed per-group top-16 maxima (gpk: group 2i in the
-// low half of gpk[i], 2i + 1 in the high half): the group maxima, and per group the lowest lane
-// holding its maximum together with the maximum over every other lane (GroupRecord).  Two
-// packed wave maxima per pair of groups; the lanes come from ballots (SALU).
+// low half of gpk[i], 2i + 1 in the high half): the group maxima (one packed wave maximum per
+// pair of groups) and the lanes whose maximum reaches the hot threshold (one ballot per group).
 template <int G>
-__device__ __forceinline__ GroupRecord tile_groups(const uint32_t (&gpk)[(G + 1) / 2]) {
-    const uint32_t lane = lane_id();
-    uint64_t gm = 0, gs = 0, g3 = 0;
-    // lowest lane whose packed half equals m's (every lane is live in the tile kernel, and m is
-    // always some remaining lane's value)
-    auto arg = [&](uint32_t v, uint32_t m, bool hi) {
-        return (uint32_t)__builtin_ctzll(__ballot(hi ? (v >> 16) == (m >> 16) : (v & 0xffffu) == (m & 0xffffu)));
-    };
-    auto drop = [&](uint32_t la, uint32_t lb) {  // clears lane la's low half and lane lb's high half
-        return (lane == la ? 0u : 0xffffu) | (lane == lb ? 0u : 0xffff0000u);
-    };
+__device__ __forceinline__ GroupRecord tile_groups(const uint32_t (&gpk)[(G + 1) / 2], uint32_t hot) {
+    GroupRecord r;
+    r.max = 0;
+    r.pad = 0;
 #pragma unroll
     for (int i = 0; i < (G + 1) / 2; ++i) {
         const uint32_t v = gpk[i];
-        const uint32_t mx = wave_max_pk16(v);
-        const uint32_t a0 = arg(v, mx, false), b0 = arg(v, mx, true);
-        const uint32_t v1 = v & drop(a0, b0);
-        const uint32_t sec = wave_max_pk16(v1);
-        gm |= (uint64_t)mx << (32 * i);
-        gs |= (uint64_t)(group_sec_field(sec & 0xffffu, a0) | group_sec_field(sec >> 16, b0) << 16) << (32 * i);
-        if constexpr (kGroupThird) {
-            const uint32_t a1 = arg(v1, sec, false), b1 = arg(v1, sec, true);
-            const uint32_t thr = wave_max_pk16(v1 & drop(a1, b1));
-            g3 |= (uint64_t)(group_sec_field(thr & 0xffffu, a1) | group_sec_field(thr >> 16, b1) << 16) << (32 * i);
-        }
+        r.max |= (uint64_t)wave_max_pk16(v) << (32 * i);
+        r.hot[2 * i] = __ballot((v & 0xffffu) >= hot);
+        r.hot[2 * i + 1] = __ballot((v >> 16) >= hot);
     }
-    return GroupRecord{gm, gs, g3, 0};
+    return r;
 }
 
 // Persistent: one 1024-thread workgroup per CU, each wave a contiguous range of tiles.
@@ -509,6 +493,7 @@ __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restri
                                                        uint64_t n_tiles,
                                                        TileRecord *__restrict__ rec,
                                                        GroupRecord *__restrict__ grp,
+                                                       uint32_t hot,
                                                        uint32_t *__restrict__ xlist,
                                                        uint32_t *__restrict__ xcount) {
     stage_tile_tables(tab);
@@ -568,7 +553,7 @@ __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restri
         uint32_t gpk[(G + 1) / 2];
         tile_scan<G>(cur, nx, x, prev_word, lb_a, lb_b, top, first, last, gpk);
         if constexpr (G > 1) {  // this tile's group bounds, stored now (no exact key needed)
-            const GroupRecord g = tile_groups<G>(gpk);
+            const GroupRecord g = tile_groups<G>(gpk, hot);
             if (lane == 0) grp[t] = g;
         }
 
@@ -661,7 +646,7 @@ __device__ __forceinline__ void exact_tile(const uint64_t *tl, const uint64_t *t
     if (lane_id() == 0) {
         rec[t].key = bk;
         rec[t].j = bj;
-        if (grp) grp[t] = GroupRecord{~0ull, 0ull, 0ull, 0ull};  // no group bounds: exact tile
+        if (grp) grp[t] = GroupRecord{~0ull, {~0ull, ~0ull, ~0ull, ~0ull}, 0ull};  // no bounds
     }
 }
 
@@ -1450,31 +1435,31 @@ __global__ __launch_bounds__(kChainWaves * 64) void rc_spec_kernel(const KeyTabl
 constexpr int kLaneFull = 8;  // widest window of the lane chain: window keys / kTileKeys <= 8
 constexpr int kLaneIters = kTileIters / kTileGroups;  // tile-kernel iterations per group
 
-// Group classification of one edge range [a, b] inside tile te, as task bits: bit q = evaluate
-// group q's lane l0, bit kTileGroups + q = its lane l1 too; sc = the groups left to an exact
-// scan (three lanes reach the best).
-__device__ __forceinline__ uint32_t lane_groups(bool live, const GroupRecord &g, uint32_t te,
-                                                uint32_t a, uint32_t b, uint32_t t16,
-                                                uint32_t &sc) {
-    uint32_t ev = 0;
+// Group classification of one edge range [a, b] inside tile te: mk[q] = the lanes of group q
+// whose keys the walking lane evaluates (its hot lanes, when the best so far reaches the hot
+// threshold, at most kLaneHotMax of them), sc = the groups left to an exact scan (below the
+// threshold, or more hot lanes); a group whose top-16 maximum is below the best needs neither.
+constexpr uint32_t kLaneHotMax = 4;
+constexpr int kLaneTasks = 2;  // (group, lane) tasks per round of the lane chain (even; 4: slower,
+                               // every slot's scan is paid whether a lane has a task or not)
+
+__device__ __forceinline__ void lane_groups(bool live, const GroupRecord &g, uint32_t te,
+                                            uint32_t a, uint32_t b, uint32_t t16, uint32_t hot,
+                                            uint64_t (&mk)[kTileGroups], uint32_t &sc) {
     sc = 0;
-    if (!live) return 0;
+#pragma unroll
+    for (int q = 0; q < kTileGroups; ++q) mk[q] = 0;
+    if (!live) return;
     const uint32_t tj0 = te * kTileKeys;
     const uint32_t qa = (a - tj0) / kGroupKeys, qb = (b - tj0) / kGroupKeys;
 #pragma unroll
-    for (uint32_t q = 0; q < (uint32_t)kTileGroups; ++q) {
-        if (q < qa || q > qb) continue;
+    for (int q = 0; q < kTileGroups; ++q) {
+        if ((uint32_t)q < qa || (uint32_t)q > qb) continue;
         if (((uint32_t)(g.max >> (16 * q)) & 0xffffu) < t16) continue;  // nothing reaches the best
-        ev |= 1u << q;                                                     // lane l0
-        if (group_sec_bound((uint32_t)(g.sec >> (16 * q)) & 0xffffu) < t16) continue;
-        if (!kGroupThird) {
-            sc |= 1u << q;
-            continue;
-        }
-        ev |= 1u << (kTileGroups + q);                                     // lane l1 as well
-        if (group_sec_bound((uint32_t)(g.third >> (16 * q)) & 0xffffu) >= t16) sc |= 1u << q;
+        const uint32_t nh = (uint32_t)__popcll(g.hot[q]);
+        if (t16 < hot || nh > kLaneHotMax || nh == 0) sc |= 1u << q;  // (nh 0: an exact tile's max)
+        else mk[q] = g.hot[q];
     }
-    return ev;
 }
 
 // top-16 of key j from the prefilter entries of its two words (gclmul.h)
@@ -1579,34 +1564,6 @@ __device__ __forceinline__ void lq_fold(const uint64_t *tl, const uint64_t *th, 
     if (c1.tie) lq_all(tl, th, base, jq1, a1, b1, bk, bj);
 }
 
-// The 6-bit lanes of a GroupRecord lane word's kTileGroups fields, one per byte.
-__device__ __forceinline__ uint32_t lane_bytes(uint64_t f) {
-    uint32_t r = 0;
-#pragma unroll
-    for (int q = 0; q < kTileGroups; ++q) r |= (uint32_t)((f >> (16 * q)) & 63u) << (8 * q);
-    return r;
-}
-
-// Pops the next of a lane's tasks (lane_groups bits: head l0 / l1 groups, then the tail's) as the
-// first key block jq of the task's lane and the range [a, b]; a > b when there is none.  hl / tl:
-// lane_bytes of the head / tail tile's sec (low half) and third (high half).  Plain values
-// throughout: a conditional between references would be a select of addresses, which LLVM
-// keeps in scratch memory.
-__device__ __forceinline__ void pop_task(uint32_t &tasks, uint64_t hl, uint64_t tl, uint32_t te0,
-                                         uint32_t te1, uint32_t a0, uint32_t b0, uint32_t a1,
-                                         uint32_t b1, uint32_t &jq, uint32_t &a, uint32_t &b) {
-    a = 1, b = 0;
-    if (!tasks) return;
-    const uint32_t bit = (uint32_t)__builtin_ctz(tasks);
-    tasks &= tasks - 1;
-    const bool tail = bit >= 2 * kTileGroups;
-    const uint32_t q = bit % kTileGroups, sh = (bit / kTileGroups & 1u) * 32 + 8 * q;
-    const uint32_t lane = (uint32_t)((tail ? tl : hl) >> sh) & 63u;
-    jq = (tail ? te1 : te0) * kTileKeys + q * kGroupKeys + 4 * lane;
-    a = tail ? a1 : a0;
-    b = tail ? b1 : b0;
-}
-
 // Best exact key over [a, b] of one stream by the whole wave, 64 * U keys per memory round trip.
 template <int U>
 __device__ __forceinline__ void scan_range(const uint64_t *tl, const uint64_t *th,
@@ -1689,8 +1646,8 @@ __global__ __launch_bounds__(256) void rc_lane_chain_kernel(const KeyTables *__r
         const bool spec = live0;
         const uint32_t lc = (s4 & 255u) >> 2, qc = (s4 & (kTileKeys - 1)) / kGroupKeys;
         const uint32_t jqc = (s4 & ~(uint32_t)(kGroupKeys - 1)) + 4 * lc;
-        LaneQuarter x0, x1;
-        lq_load(base, jqc, spec ? a0 : 1u, spec ? b0 : 0u, x0);
+        LaneQuarter x[kLaneTasks];
+        lq_load(base, jqc, spec ? a0 : 1u, spec ? b0 : 0u, x[0]);
 
         uint64_t bk = 0;
         uint32_t bj = ~0u;
@@ -1711,41 +1668,70 @@ __global__ __launch_bounds__(256) void rc_lane_chain_kernel(const KeyTables *__r
         }
         uint32_t sc0, sc1;
         RC_LSTAMP(2);
-        // tasks: bits 0..2G-1 the head's (lane l0 of group q, then lane l1), 2G.. the tail's
-        uint32_t tasks = lane_groups(live0, g0, te0, a0, b0, (uint32_t)(bk >> 48), sc0);
-        tasks |= lane_groups(live1, g1, te1, a1, b1, (uint32_t)(bk >> 48), sc1) << (2 * kTileGroups);
-        // the tasks' lanes, one byte per group: head l0 / l1, tail l0 / l1
-        const uint64_t hl = (uint64_t)lane_bytes(g0.third) << 32 | lane_bytes(g0.sec);
-        const uint64_t tll = (uint64_t)lane_bytes(g1.third) << 32 | lane_bytes(g1.sec);
+        // tasks: the (group, lane) pairs to evaluate, as lane masks per group of the head's tile
+        // (h) and the tail's (t), popped head first
+        uint64_t h[kTileGroups], t[kTileGroups];
+        lane_groups(live0, g0, te0, a0, b0, (uint32_t)(bk >> 48), prm.hot, h, sc0);
+        lane_groups(live1, g1, te1, a1, b1, (uint32_t)(bk >> 48), prm.hot, t, sc1);
+        static_assert(kTileGroups == 4, "the task queue below spells out four groups");
+        auto any_task = [&]() { return (h[0] | h[1] | h[2] | h[3] | t[0] | t[1] | t[2] | t[3]) != 0; };
+        // pops the next task as its lane's first key block jq and range [a, b] (a > b: none)
         auto task = [&](uint32_t &jq, uint32_t &a, uint32_t &b) {
-            pop_task(tasks, hl, tll, te0, te1, a0, b0, a1, b1, jq, a, b);
+            int r = -1;
+            uint32_t q = 0, l = 0;
+#define RC_POP(M, R, Q)                            \
+    if (r < 0 && M) {                              \
+        l = (uint32_t)__builtin_ctzll(M);          \
+        M &= M - 1;                                \
+        r = R;                                     \
+        q = Q;                                     \
+    }
+            RC_POP(h[0], 0, 0) RC_POP(h[1], 0, 1) RC_POP(h[2], 0, 2) RC_POP(h[3], 0, 3)
+            RC_POP(t[0], 1, 0) RC_POP(t[1], 1, 1) RC_POP(t[2], 1, 2) RC_POP(t[3], 1, 3)
+#undef RC_POP
+            a = 1, b = 0;
+            if (r < 0) return;
+            jq = (r ? te1 : te0) * kTileKeys + q * kGroupKeys + 4 * l;
+            a = r ? a1 : a0;
+            b = r ? b1 : b0;
         };
 
-        // the lanes' keys, two tasks per round with their loads in flight together.  The
-        // first is, as a rule, the previous cut's own group and lane (that cut's key is the
+        // the lanes' keys, kLaneTasks tasks per round with their loads in flight together.
+        // The first is, as a rule, the previous cut's own group and lane (that cut's key is the
         // maximum of the previous window): its words came with the records.
-        bool first = spec && (tasks >> qc & 1u) && ((uint32_t)(hl >> (8 * qc)) & 63u) == lc;
-        if (first) tasks &= ~(1u << qc);
-        uint32_t jq0 = jqc, ha = first ? a0 : 1u, hb = first ? b0 : 0u;
+        bool first = false;
+#define RC_FIRST(Q)                                              \
+    if (spec && qc == Q && (h[Q] >> lc & 1u)) {                  \
+        h[Q] &= ~(1ull << lc);                                   \
+        first = true;                                            \
+    }
+        RC_FIRST(0) RC_FIRST(1) RC_FIRST(2) RC_FIRST(3)
+#undef RC_FIRST
+        uint32_t jq[kLaneTasks], ra[kLaneTasks], rb[kLaneTasks];
+        jq[0] = jqc, ra[0] = first ? a0 : 1u, rb[0] = first ? b0 : 0u;
         for (;;) {
-            if (!__any(first || tasks != 0)) break;
-            if (!first) {
-                task(jq0, ha, hb);
-                lq_load(base, jq0, ha, hb, x0);
+            if (!__any(first || any_task())) break;
+#pragma unroll
+            for (int k = 0; k < kLaneTasks; ++k) {
+                if (k == 0 && first) continue;  // x[0] holds the previous cut's lane already
+                task(jq[k], ra[k], rb[k]);
+                lq_load(base, jq[k], ra[k], rb[k], x[k]);
             }
-            uint32_t jq1 = 0, ta, tb;
-            task(jq1, ta, tb);
-            lq_load(base, jq1, ta, tb, x1);
             const uint32_t t16 = (uint32_t)(bk >> 48);
-            const LaneCand c0 = lq_scan(pf, x0, jq0, ha, hb, t16);
-            const LaneCand c1 = lq_scan(pf, x1, jq1, ta, tb, t16);
-            lq_fold(tl, th, base, c0, jq0, ha, hb, c1, jq1, ta, tb, bk, bj);
+            LaneCand c[kLaneTasks];
+#pragma unroll
+            for (int k = 0; k < kLaneTasks; ++k) c[k] = lq_scan(pf, x[k], jq[k], ra[k], rb[k], t16);
+#pragma unroll
+            for (int k = 0; k < kLaneTasks; k += 2)
+                lq_fold(tl, th, base, c[k], jq[k], ra[k], rb[k], c[k + 1], jq[k + 1], ra[k + 1],
+                        rb[k + 1], bk, bj);
             first = false;
             RC_LSTAMP(3);
         }
         RC_LSTAMP(4);
 
-        // groups three lanes reach: exact scans by the whole wave, one lane's range at a time
+        // groups with too many hot lanes, or a best below the threshold: exact scans by the whole
+        // wave, one lane's range at a time
         // (from the first to the last such group of the range), a group per memory round trip
 #pragma unroll 1
         for (int r = 0; r < 2; ++r) {
@@ -2217,7 +2203,7 @@ int rc_diag_read(uint64_t *out, uint32_t cap, uint32_t *n) {
 
 int rc_launch_tiles(const KeyTables *d_tables, StreamDesc desc, uint64_t n_streams,
                     uint64_t n_tiles, TileRecord *d_records, GroupRecord *d_grp,
-                    uint32_t *d_xlist, void *stream, void *mid_event) {
+                    uint32_t hot, uint32_t *d_xlist, void *stream, void *mid_event) {
     hipStream_t st = (hipStream_t)stream;
     if (n_tiles == 0) {
         if (mid_event && hipEventRecord((hipEvent_t)mid_event, st) != hipSuccess) return 1;
@@ -2232,11 +2218,11 @@ int rc_launch_tiles(const KeyTables *d_tables, StreamDesc desc, uint64_t n_strea
     const uint64_t n_waves = grid * waves_per_wg;
     if (d_grp)
         hipLaunchKernelGGL(rc_tile_kernel<kTileGroups>, dim3((unsigned)grid), dim3(1024), 0, st,
-                           d_tables, desc, n_streams, n_tiles, d_records, d_grp, d_xlist,
+                           d_tables, desc, n_streams, n_tiles, d_records, d_grp, hot, d_xlist,
                            d_xcount);
     else
         hipLaunchKernelGGL(rc_tile_kernel<1>, dim3((unsigned)grid), dim3(1024), 0, st, d_tables,
-                           desc, n_streams, n_tiles, d_records, d_grp, d_xlist, d_xcount);
+                           desc, n_streams, n_tiles, d_records, d_grp, hot, d_xlist, d_xcount);
     if (launch_status("rc_tile_kernel")) return 1;
     if (mid_event && hipEventRecord((hipEvent_t)mid_event, st) != hipSuccess) {
         snprintf(g_launch_err, sizeof g_launch_err, "hipEventRecord failed");

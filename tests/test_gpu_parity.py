@@ -277,10 +277,10 @@ def test_tile_records_vs_oracle(kind):
 
 @pytest.mark.parametrize('kind', ['random', 'zeros', 'periodic', 'seeded_key'])
 def test_tile_group_maxima_vs_oracle(kind):
-    """Small-window chunkers: the tile kernel's per-quarter group bounds (top-16 maxima, the
-    maximum's lane and the maximum over the other lanes, the runner-up's lane and the maximum
-    over the rest) equal the oracle's for every fast tile; a tile sent to the exact path (the stream ends inside it, or a tie) reports ~0, the
-    no-bound value."""
+    """Small-window chunkers: the tile kernel's per-quarter group bounds (top-16 maxima and the
+    lanes holding a key at or above the hot threshold) equal the oracle's for every fast tile;
+    a tile sent to the exact path (the stream ends inside it, or a tie) reports ~0 and every
+    lane hot, the no-bound values."""
     o = _oracle()
     from replicat_amd.chunker import keys_needed, tile_keys
     tk = tile_keys()
@@ -297,7 +297,8 @@ def test_tile_group_maxima_vs_oracle(kind):
         datas = [synth.stream_bytes(n, synth.DEFAULT_SEED, 300 + i) for i, n in enumerate(sizes)]
     last = [0, (1 << 20) - 100, 0, 0]
     ts = device_streams(sizes, datas=datas)
-    keys, js, gm, gs, g3 = ch.tile_records([t.data_ptr() for t in ts], sizes, last, groups=True)
+    keys, js, gm, gh, hot = ch.tile_records([t.data_ptr() for t in ts], sizes, last, groups=True)
+    assert 60000 < hot < 65536  # max 80,000: a window of 19,999 keys
     k0 = int.from_bytes(key[:8], 'little')
     k1 = int.from_bytes(key[8:], 'little')
     base = exact = 0
@@ -306,16 +307,14 @@ def test_tile_group_maxima_vs_oracle(kind):
         jneed = keys_needed(mx, n, P)
         nt = jneed // tk + 1 if jneed else 0
         eg = np.zeros(max(nt, 1), np.uint64)
-        es = np.zeros(max(nt, 1), np.uint64)
-        e3 = np.zeros(max(nt, 1), np.uint64)
+        eh = np.zeros((max(nt, 1), 4), np.uint64)
         buf = np.concatenate([d, np.zeros(16, np.uint8)])
         o.lib().oc_tile_groups(k0, k1, buf.ctypes.data, n, tk, nt, 4, eg.ctypes.data)
-        o.lib().oc_tile_groups_sec(k0, k1, buf.ctypes.data, n, tk, nt, 4, es.ctypes.data,
-                                   e3.ctypes.data)
-        g, s, s3 = gm[base:base + nt], gs[base:base + nt], g3[base:base + nt]
+        o.lib().oc_tile_groups_hot(k0, k1, buf.ctypes.data, n, tk, nt, 4, hot, eh.ctypes.data)
+        g, h = gm[base:base + nt], gh[base:base + nt]
         computed = g != none  # a tile sent to the exact path has no bounds at all
-        ok = (((g == eg[:nt]) & (s == es[:nt]) & (s3 == e3[:nt])) |
-              (~computed & (s == 0) & (s3 == 0)))
+        ok = (((g == eg[:nt]) & (h == eh[:nt]).all(axis=1)) |
+              (~computed & (h == none).all(axis=1)))
         assert ok.all(), (kind, n, np.nonzero(~ok)[0][:8].tolist())
         exact += int((~computed & (eg[:nt] != none)).sum())
         base += nt
