@@ -477,7 +477,9 @@ class Config3ii:
         self.ends = None
         self.rounds = 0
 
-    def chunk_window(self, w, entry):
+    def enqueue(self, w, entry):
+        """Chunk window w from ``entry`` on the device (cut ends relative to entry in
+        self.cuts / the returned tensor); enqueue only."""
         off = entry - w.start
         src, n = self.buf.data_ptr() + off, w.end - entry
         tmp = None
@@ -489,13 +491,52 @@ class Config3ii:
         cuts = self.cuts if int(caps[0]) <= self.cap else self.be.zeros_i64(int(caps[0]))
         self.ch.chunk_device([src], [n], [max(0, w.last_piece - off) if not w.open else 0],
                              cuts.data_ptr(), self.counts.data_ptr(), self.hs, open_=w.open)
+        self._tmp = tmp
+        return cuts
+
+    def chunk_window(self, w, entry):
+        """The whole cut list of window w from ``entry``, absolute, on the host."""
+        cuts = self.enqueue(w, entry)
         c = int(self.counts.cpu()[0])
         return (cuts[:c].cpu().numpy() + entry).tolist()
 
+    EXCHANGE = 64  # cut ends of each window's head and tail in the compact exchange
+
     def step(self):
+        """One GPU: the stream is chunked on the device and its cuts stay there.  Several: each
+        rank chunks its window, and the ranks exchange only the first and last EXCHANGE cuts of
+        their chains (a host gather of a few KB) to find where the true chain meets each
+        window's speculative one -- the whole lists only when that fails (split.chunk_split)."""
         from replicat_amd import split
-        self.ends, self.rounds = split.chunk_split(self.chunk_window, self.windows, self.rank,
-                                                   self.ranks.gather)
+        self.ends, self._bounds = None, None
+        cuts = self.enqueue(self.w, self.w.start)
+        self._cuts = cuts
+        if self.world == 1:
+            return
+        c = int(self.counts.cpu()[0])
+        k = self.EXCHANGE
+        head = (cuts[:min(c, k)].cpu().numpy() + self.w.start).tolist()
+        tail = (cuts[max(0, c - k):c].cpu().numpy() + self.w.start).tolist()
+        bounds = split.merge_points(self.windows, self.ranks.gather((self.w.start, head, tail)))
+        if bounds is None:
+            self.ends, self.rounds = split.chunk_split(self.chunk_window, self.windows, self.rank,
+                                                       self.ranks.gather)
+            return
+        self._bounds = bounds
+
+    def finish(self):
+        """The whole true cut list on every rank (parity; outside the timed region)."""
+        if self.ends is not None:
+            return
+        c = int(self.counts.cpu()[0])
+        mine = (self._cuts[:c].cpu().numpy() + self.w.start).tolist()
+        if self.world == 1:
+            self.ends = mine
+            return
+        lo = self._bounds[self.rank]
+        hi = self._bounds[self.rank + 1] if self.rank + 1 < self.world else None
+        part = [p for p in mine if p > lo and (hi is None or p <= hi)]
+        self.ends = [p for prt in self.ranks.gather(part) for p in prt]
 
 
 # ------------------------------------------------------------------------------ main
@@ -664,6 +705,7 @@ def main(argv=None, backend=Backend):
     parity, ends, scope = None, None, None
     if not args.no_verify:
         if long is not None:
+            long.finish()
             ends = [np.asarray(long.ends, dtype=np.uint64)]
             digest = _golden().cutlist_digest(ends)
         else:

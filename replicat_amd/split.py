@@ -85,3 +85,25 @@ def chunk_split(chunk_window, windows, rank, gather):
         rounds += 1
         mine = (entry, chunk_window(windows[r], entry)) if rank == r else None
         chains[r] = gather(mine)[r]
+
+
+def merge_points(windows, info):
+    """Slice bounds from a compact exchange: ``info[r] = (entry, head, tail)`` with ``head`` the
+    first cut ends of window r's chain from ``entry`` and ``tail`` its last ones (absolute).
+    Returns ``bounds`` (rank r keeps its cuts p with bounds[r] < p <= bounds[r + 1], the last
+    rank to its end), or None when a boundary cannot be settled from the exchanged cuts (the
+    caller then runs chunk_split).  At boundary r the true chain, followed in window r - 1's
+    tail, meets window r's speculative chain at a position both hold: from there they are the
+    same chain, so any common position after window r - 1's own merge is a valid splice."""
+    bounds = [0]
+    for r in range(1, len(windows)):
+        entry, head, _ = info[r]
+        spec = {int(entry)}
+        spec.update(int(p) for p in head)
+        tail_prev = [int(p) for p in info[r - 1][2]]
+        p = next((t for t in tail_prev if t >= entry and t in spec and t > bounds[-1]), None)
+        if p is None:
+            return None
+        bounds.append(p)
+    return bounds
+

@@ -169,3 +169,31 @@ def test_chunk_split_gloo_two_ranks():
     data = synth.stream_bytes(L, synth.DEFAULT_SEED, 5)
     exp = o.chunk_stream(data, 500, 10_000, synth.seeded_key(9), L - 4_096)
     assert res[0][1] == exp and res[1][1] == exp
+
+
+@pytest.mark.parametrize('world', [2, 3, 5])
+@pytest.mark.parametrize('k', [4, 64])
+def test_merge_points_compact_exchange(world, k):
+    """bench.py's compact exchange: from each window's first and last k cut ends alone, the
+    slice bounds reproduce the whole stream's cut list (or ask for the full protocol)."""
+    o = _oracle()
+    mn, mx = 500, 10_000
+    key = synth.seeded_key(world)
+    L = 600_000 + 13 * world
+    data = synth.stream_bytes(L, synth.DEFAULT_SEED, 70 + world)
+    P = L - 7_000
+    windows = split.plan_windows(L, P, world, mx)
+    fn = oracle_window(data, mn, mx, key)
+    lists = [fn(w, w.start) for w in windows]
+    info = [(w.start, c[:k], c[-k:]) for w, c in zip(windows, lists)]
+    bounds = split.merge_points(windows, info)
+    if bounds is None:  # 4 cuts need not span the halo (~8 chunks here): the caller falls back
+        assert k == 4
+        return
+    ends = []
+    for r, c in enumerate(lists):
+        hi = bounds[r + 1] if r + 1 < world else None
+        ends += [p for p in c if p > bounds[r] and (hi is None or p <= hi)]
+    assert ends == o.chunk_stream(data, mn, mx, key, P)
+    # nothing exchanged past the entries: no bounds, the caller falls back
+    assert split.merge_points(windows, [(w.start, [], []) for w in windows]) is None
