@@ -416,10 +416,14 @@ int upload_and_launch(rc_chunker *ch, Workspace &ws, const Plan &plan, ChainPara
     prm.grp = grp;
     prm.n_tiles = plan.n_tiles;
     // lane-per-stream chain (kernels.hip rc_lane_chain_kernel) for batches of many streams;
-    // RC_LANE_CHAIN=0 never, =1 whatever the count (read per call: tests switch it)
+    // RC_LANE_CHAIN=0 never, =1 whatever the count, =lane one lane per stream instead of a quad
+    // (read per call: tests switch it)
     {
         const char *e = getenv("RC_LANE_CHAIN");
-        prm.lane = e && e[0] == '0' ? 0u : (e && e[0] == '1') ? 2u : plan.n >= kLaneMinStreams ? 1u : 0u;
+        prm.lane = e && e[0] == '0'   ? 0u
+                   : e && e[0] == '1' ? 2u
+                   : e && e[0] == 'l' ? 3u  // "lane": one lane per stream instead of a quad
+                   : plan.n >= kLaneMinStreams ? 1u : 0u;
     }
     // 32-bit chain steps: small windows (the one-row record cache) and key indices < 2^32
     prm.lean = ch->small && plan.max_len < (16ull << 30) ? 1u : 0u;

@@ -1799,6 +1799,307 @@ __global__ __launch_bounds__(256) void rc_lane_chain_kernel(const KeyTables *__r
     if (mine) counts[s] = overflow ? -1 : (int64_t)n;
 }
 
+// ---- the quad-per-stream chain: the lane chain with four lanes per stream
+//
+// The lane chain runs one wave per SIMD on config 3 (iii) (65,536 lanes), so a step is ~14 us
+// of mostly dependent instructions with nothing to overlap them.  Here a QUAD of lanes walks
+// each stream: the steps are the same, but lane q of the quad loads the window's full-tile
+// record q (and q + 4) and takes iteration q of every (group, lane) task -- one 16-byte block,
+// the word before it and 4 keys, not 4 of each -- and the quad reduces records and candidates
+// with two DPP quad_perm exchanges.  Four waves per SIMD hide each other's latency.
+template <int kCtrl>
+__device__ __forceinline__ uint32_t qperm32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kCtrl, 0xf, 0xf, true);
+}
+template <int kCtrl>
+__device__ __forceinline__ uint64_t qperm64(uint64_t v) {
+    return (uint64_t)qperm32<kCtrl>((uint32_t)(v >> 32)) << 32 | qperm32<kCtrl>((uint32_t)v);
+}
+// (key desc, index asc) best over the quad, in every lane of it
+__device__ __forceinline__ void quad_best32(uint64_t &k, uint32_t &j) {
+    {
+        const uint64_t ko = qperm64<0xB1>(k);  // quad_perm [1, 0, 3, 2]
+        const uint32_t jo = qperm32<0xB1>(j);
+        if (ko > k || (ko == k && jo < j)) k = ko, j = jo;
+    }
+    {
+        const uint64_t ko = qperm64<0x4E>(k);  // quad_perm [2, 3, 0, 1]
+        const uint32_t jo = qperm32<0x4E>(j);
+        if (ko > k || (ko == k && jo < j)) k = ko, j = jo;
+    }
+}
+
+// One quad lane's iteration of a task: keys j4 .. j4 + 3 of the task's lane, j4 = jq + 256 q.
+struct QuadIter {
+    u32x4 v;     // the block
+    uint32_t p;  // the word before it
+};
+
+__device__ __forceinline__ QuadIter qi_load(const uint8_t *base, uint32_t j4, uint32_t a,
+                                            uint32_t b) {
+    QuadIter x = {u32x4{0u, 0u, 0u, 0u}, 0u};
+    if (j4 <= b && j4 + 3 >= a) {  // a block holding a key <= b <= jmax cannot cross a page
+        x.v = *as_global_x4(base + 4ull * j4);
+        x.p = ld_u32(base + 4ull * j4 - (j4 ? 4 : 0));
+    }
+    return x;
+}
+
+// Folds the iteration's keys in [a, b] whose top-16 value reaches t16 into (lk, lj): the exact
+// key of the one with the largest top-16 value, or of all of them when two share it (rare).
+__device__ __forceinline__ void qi_eval(const uint32_t *pf, const uint64_t *tl, const uint64_t *th,
+                                        const uint8_t *base, const QuadIter &x, uint32_t j4,
+                                        uint32_t a, uint32_t b, uint32_t t16, uint64_t &lk,
+                                        uint32_t &lj) {
+    if (!(j4 <= b && j4 + 3 >= a)) return;
+    const uint32_t wd[5] = {x.p, x.v.x, x.v.y, x.v.z, x.v.w};
+    uint32_t e[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) e[k] = pfc_entry(pf, wd[k]);
+    bool have = false, tie = false;
+    uint32_t ct = 0, cj = 0, clo = 0, chi = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t j = j4 + k, t = top16_of(e[k], e[k + 1]);
+        const bool in = j >= a && j <= b && t >= t16;
+        const bool take = in && (!have || t > ct);
+        tie = take ? false : (tie || (in && t == ct));
+        ct = take ? t : ct;
+        cj = take ? j : cj;
+        clo = take ? wd[k] : clo;
+        chi = take ? wd[k + 1] : chi;
+        have = have || in;
+    }
+    if (have) take_best32(full_key(tl, th, clo, chi), cj, lk, lj);
+    if (tie) {
+#pragma unroll 1
+        for (uint32_t k = 0; k < 4; ++k) {
+            const uint32_t j = j4 + k;
+            if (j >= a && j <= b)
+                take_best32(full_key(tl, th, ld_u32(base + 4ull * j - 4), ld_u32(base + 4ull * j)), j, lk, lj);
+        }
+    }
+}
+
+constexpr int kQuadTasks = 4;  // (group, lane) tasks per round of the quad chain
+
+template <int F>  // full tiles per window (window keys / kTileKeys <= F; F / 4 records per lane)
+__global__ __launch_bounds__(256) void rc_quad_chain_kernel(const KeyTables *__restrict__ tab,
+                                                            StreamDesc d, uint64_t n_streams,
+                                                            ChainParams prm,
+                                                            const TileRecord *__restrict__ rec,
+                                                            uint64_t *__restrict__ cuts,
+                                                            int64_t *__restrict__ counts) {
+    static_assert(F % 4 == 0 && kLaneIters == 4, "a quad lane per record row and per iteration");
+    stage_chain_tables(tab);
+    const uint32_t *pf = s_chain_lds;
+    const uint64_t *full = reinterpret_cast<const uint64_t *>(s_chain_lds + 1024);
+    const uint64_t *tl = full, *th = full + 1024;
+    const uint32_t lane = lane_id(), q = lane & 3u;
+    const uint64_t gid = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 2;  // the stream
+    if (gid - (lane >> 2) >= n_streams) return;  // the whole wave is past the last stream
+    const bool mine = gid < n_streams;
+    const uint64_t s = mine ? gid : n_streams - 1;  // surplus quads shadow the last stream, silent
+    const GroupRecord *grp = prm.grp;
+    const uint8_t *base = d.ptr[s];
+    const uint64_t L = d.len[s], P = d.last[s];
+    const uint64_t tb0 = d.tile_base[s], nt = d.tile_base[s + 1] - tb0;
+    uint64_t *out = cuts + d.cut_base[s];
+    const uint64_t cap = d.cut_cap[s];
+    const uint32_t jmax = L >= 8 ? (uint32_t)((L - 4) / 4) : 0u;
+    const uint32_t minl = (uint32_t)prm.min_length, maxl = (uint32_t)prm.max_length;
+    const uint32_t T = (uint32_t)prm.window;
+    auto gtile = [&](bool use, uint32_t t) -> uint64_t { return use && t < nt ? tb0 + t : prm.n_tiles; };
+
+    uint64_t pos = 0, n = 0;
+    bool walking = mine && L > 0 && prm.max_steps > 0, overflow = false;
+#ifdef RC_DIAG_STAMPS
+    const bool diag = gid < 16 && q == 0;  // wave 0 (diagnostic build only)
+#endif
+    for (;;) {
+        if (!__any(walking)) break;
+        RC_LSTAMP(1);
+        const uint64_t rem = L - pos;
+        const bool argmax = (P >= pos && P - pos >= maxl) || rem >= 2ull * maxl;
+        const uint32_t s4 = (uint32_t)(pos >> 2);
+        const uint32_t ja = s4 + 1, jb = min(s4 + T, jmax);
+        const bool win = walking && argmax && T > 0 && ja <= jb;
+        const uint32_t t_lo = (ja + kTileKeys - 1) / kTileKeys, t_hi = (jb + 1) / kTileKeys;
+        const uint32_t nf = win && t_hi > t_lo ? t_hi - t_lo : 0u;
+        const uint32_t a0 = ja, b0 = min(jb, t_lo * kTileKeys - 1), te0 = ja / kTileKeys;
+        const uint32_t a1 = t_hi * kTileKeys, b1 = jb, te1 = t_hi;
+        bool live0 = win && ja < t_lo * kTileKeys;
+        bool live1 = win && t_hi >= t_lo && jb >= a1;
+
+        TileRecord fr[F / 4];
+#pragma unroll
+        for (int i = 0; i < F / 4; ++i) {
+            const uint32_t t = 4 * i + q;
+            fr[i] = rec[gtile(t < nf, t_lo + t)];
+        }
+        const TileRecord r0 = rec[gtile(live0, te0)], r1 = rec[gtile(live1, te1)];
+        const GroupRecord g0 = grp[gtile(live0, te0)], g1 = grp[gtile(live1, te1)];
+        // the previous cut's lane in its group: iteration q of it
+        const bool spec = live0;
+        const uint32_t lc = (s4 & 255u) >> 2, qc = (s4 & (kTileKeys - 1)) / kGroupKeys;
+        const uint32_t jqc = (s4 & ~(uint32_t)(kGroupKeys - 1)) + 4 * lc;
+        QuadIter x[kQuadTasks];
+        x[0] = qi_load(base, jqc + 256 * q, spec ? a0 : 1u, spec ? b0 : 0u);
+
+        uint64_t bk = 0;
+        uint32_t bj = ~0u;
+#pragma unroll
+        for (int i = 0; i < F / 4; ++i)
+            if (4 * (uint32_t)i + q < nf && fr[i].key != 0) take_best32(fr[i].key, (uint32_t)fr[i].j, bk, bj);
+        quad_best32(bk, bj);
+        if (live0) {
+            const uint32_t rj = (uint32_t)r0.j;
+            const bool inr = r0.key != 0 && rj >= a0 && rj <= b0;
+            if (inr) take_best32(r0.key, rj, bk, bj);
+            if (r0.key == 0 || inr || r0.key < bk) live0 = false;
+        }
+        if (live1) {
+            const uint32_t rj = (uint32_t)r1.j;
+            const bool inr = r1.key != 0 && rj >= a1 && rj <= b1;
+            if (inr) take_best32(r1.key, rj, bk, bj);
+            if (r1.key == 0 || inr || r1.key <= bk) live1 = false;
+        }
+        uint32_t sc0, sc1;
+        RC_LSTAMP(2);
+        uint64_t h[kTileGroups], t[kTileGroups];
+        lane_groups(live0, g0, te0, a0, b0, (uint32_t)(bk >> 48), prm.hot, h, sc0);
+        lane_groups(live1, g1, te1, a1, b1, (uint32_t)(bk >> 48), prm.hot, t, sc1);
+        static_assert(kTileGroups == 4, "the task queue below spells out four groups");
+        auto any_task = [&]() { return (h[0] | h[1] | h[2] | h[3] | t[0] | t[1] | t[2] | t[3]) != 0; };
+        auto task = [&](uint32_t &jq, uint32_t &a, uint32_t &b) {
+            int r = -1;
+            uint32_t g = 0, l = 0;
+#define RC_POP(M, R, Q)                            \
+    if (r < 0 && M) {                              \
+        l = (uint32_t)__builtin_ctzll(M);          \
+        M &= M - 1;                                \
+        r = R;                                     \
+        g = Q;                                     \
+    }
+            RC_POP(h[0], 0, 0) RC_POP(h[1], 0, 1) RC_POP(h[2], 0, 2) RC_POP(h[3], 0, 3)
+            RC_POP(t[0], 1, 0) RC_POP(t[1], 1, 1) RC_POP(t[2], 1, 2) RC_POP(t[3], 1, 3)
+#undef RC_POP
+            a = 1, b = 0;
+            if (r < 0) return;
+            jq = (r ? te1 : te0) * kTileKeys + g * kGroupKeys + 4 * l;
+            a = r ? a1 : a0;
+            b = r ? b1 : b0;
+        };
+        bool first = false;
+#define RC_FIRST(Q)                                              \
+    if (spec && qc == Q && (h[Q] >> lc & 1u)) {                  \
+        h[Q] &= ~(1ull << lc);                                   \
+        first = true;                                            \
+    }
+        RC_FIRST(0) RC_FIRST(1) RC_FIRST(2) RC_FIRST(3)
+#undef RC_FIRST
+        uint32_t jq[kQuadTasks], ra[kQuadTasks], rb[kQuadTasks];
+        jq[0] = jqc, ra[0] = first ? a0 : 1u, rb[0] = first ? b0 : 0u;
+        for (;;) {
+            if (!__any(first || any_task())) break;
+            bool used[kQuadTasks];  // wave-uniform: a slot no quad of the wave fills is skipped
+#pragma unroll
+            for (int k = 0; k < kQuadTasks; ++k) {
+                if (!(k == 0 && first)) {  // x[0] may hold the previous cut's lane already
+                    task(jq[k], ra[k], rb[k]);
+                    x[k] = qi_load(base, jq[k] + 256 * q, ra[k], rb[k]);
+                }
+                used[k] = __any(ra[k] <= rb[k]);
+            }
+            const uint32_t t16 = (uint32_t)(bk >> 48);
+            uint64_t lk = 0;
+            uint32_t lj = ~0u;
+#pragma unroll
+            for (int k = 0; k < kQuadTasks; ++k)
+                if (used[k]) qi_eval(pf, tl, th, base, x[k], jq[k] + 256 * q, ra[k], rb[k], t16, lk, lj);
+            quad_best32(lk, lj);
+            if (lk != 0) take_best32(lk, lj, bk, bj);
+            first = false;
+            RC_LSTAMP(3);
+        }
+        RC_LSTAMP(4);
+
+        // groups with too many hot lanes, or a best below the threshold: exact scans by the whole
+        // wave, one stream's range at a time (ballot over the quads' first lanes)
+#pragma unroll 1
+        for (int r = 0; r < 2; ++r) {
+            const uint32_t sv = r == 0 ? +sc0 : +sc1;
+            const uint32_t te = r == 0 ? +te0 : +te1, ra_ = r == 0 ? +a0 : +a1, rb_ = r == 0 ? +b0 : +b1;
+            uint32_t sa = 1, sb = 0;
+            if (sv) {
+                const uint32_t qlo = (uint32_t)__builtin_ctz(sv), qhi = 31u - (uint32_t)__builtin_clz(sv);
+                sa = max(ra_, te * kTileKeys + qlo * kGroupKeys);
+                sb = min(rb_, te * kTileKeys + (qhi + 1) * kGroupKeys - 1);
+            }
+            for (uint64_t m = __ballot(q == 0 && sa <= sb); m; m &= m - 1) {
+                const int l = __builtin_ctzll(m);
+                const uint32_t la = (uint32_t)__builtin_amdgcn_readlane(sa, l);
+                const uint32_t lb = (uint32_t)__builtin_amdgcn_readlane(sb, l);
+                const uint8_t *lbase = reinterpret_cast<const uint8_t *>(lane_u64((uint64_t)base, l));
+                uint64_t ek = 0, ej = ~0ull;
+                scan_range<kGroupKeys / 64>(tl, th, lbase, la, lb, ek, ej);
+                wave_best(ek, ej);
+                if ((lane >> 2) == ((uint32_t)l >> 2) && ek != 0) take_best32(ek, (uint32_t)ej, bk, bj);
+                RC_LSTAMP(5);
+            }
+        }
+        RC_LSTAMP(6);
+
+        // the step's cut(s), the same in the four lanes; lane 0 of the quad stores them
+        if (walking) {
+            int kind = kStepStop;
+            uint64_t c1 = 0, c2 = 0;
+            if (argmax) {
+                uint32_t idx = bk > 0 ? 4u * (bj - s4) : 0u;
+                if (idx < minl) idx = (minl + 3) & ~3u;  // adapters.cpp:66-67
+                if (idx != 0) {
+                    c1 = pos + idx;
+                    kind = kStepCut;
+                }
+            }
+            if (kind != kStepCut && !prm.open && !(argmax && rem >= 2ull * maxl)) {
+                uint64_t c;  // the tail rule (adapters.cpp:48-55); argmax with idx 0 is S7 UB
+                if (rem <= maxl) c = rem;
+                else if (rem < (uint64_t)maxl + minl) c = rem / 2;
+                else c = maxl;
+                if (c != 0) {
+                    c1 = pos + c;
+                    kind = kStepTail1;
+                    if (c < rem) {
+                        c2 = L;
+                        kind = kStepTail2;
+                    }
+                }
+            }
+            if (kind != kStepStop) {
+                if (n < cap) {
+                    if (q == 0) out[n] = c1;
+                    ++n;
+                } else {
+                    overflow = true;
+                }
+                if (kind == kStepTail2) {
+                    if (n < cap) {
+                        if (q == 0) out[n] = c2;
+                        ++n;
+                    } else {
+                        overflow = true;
+                    }
+                }
+            }
+            if (kind != kStepCut || overflow) walking = false;
+            pos = c1;
+            if (pos >= L || n >= prm.max_steps) walking = false;
+        }
+    }
+    if (mine && q == 0) counts[s] = overflow ? -1 : (int64_t)n;
+}
+
 // ---- parallel join of the speculative lists (multi-segment streams)
 //
 // Three small launches instead of one wave walking every segment of a stream in turn (one
@@ -2247,14 +2548,25 @@ int rc_launch_chain(const KeyTables *d_tables, StreamDesc desc, uint64_t n_strea
     // many single-segment streams with small windows and group bounds: one lane per stream
     if (prm.lane && prm.lean && prm.grp && !any_multi && n_segs == n_streams &&
         prm.max_steps != 0 && prm.window / kTileKeys <= (uint64_t)kLaneFull) {
-        const uint64_t grid = (n_streams + 255) / 256;
-        if (prm.window / kTileKeys <= 4)
-            hipLaunchKernelGGL(rc_lane_chain_kernel<4>, dim3((unsigned)grid), dim3(256), 0, st,
+        const bool narrow = prm.window / kTileKeys <= 4;
+        if (prm.lane == 3) {  // RC_LANE_CHAIN=lane: one lane per stream (comparison)
+            const uint64_t grid = (n_streams + 255) / 256;
+            if (narrow)
+                hipLaunchKernelGGL(rc_lane_chain_kernel<4>, dim3((unsigned)grid), dim3(256), 0, st,
+                                   d_tables, desc, n_streams, prm, d_records, d_cuts, d_counts);
+            else
+                hipLaunchKernelGGL(rc_lane_chain_kernel<kLaneFull>, dim3((unsigned)grid), dim3(256),
+                                   0, st, d_tables, desc, n_streams, prm, d_records, d_cuts, d_counts);
+            return launch_status("rc_lane_chain_kernel");
+        }
+        const uint64_t grid = (n_streams + 63) / 64;  // a quad of lanes per stream
+        if (narrow)
+            hipLaunchKernelGGL(rc_quad_chain_kernel<4>, dim3((unsigned)grid), dim3(256), 0, st,
                                d_tables, desc, n_streams, prm, d_records, d_cuts, d_counts);
         else
-            hipLaunchKernelGGL(rc_lane_chain_kernel<kLaneFull>, dim3((unsigned)grid), dim3(256), 0,
+            hipLaunchKernelGGL(rc_quad_chain_kernel<kLaneFull>, dim3((unsigned)grid), dim3(256), 0,
                                st, d_tables, desc, n_streams, prm, d_records, d_cuts, d_counts);
-        return launch_status("rc_lane_chain_kernel");
+        return launch_status("rc_quad_chain_kernel");
     }
     // 4-wave workgroups on 20 KiB of LDS (compact tables)
     const bool small = prm.window / kTileKeys + 3 <= 64;  // window + both edge tiles in one row

@@ -1,8 +1,9 @@
-"""GPU parity of the lane-per-stream chain (kernels.hip rc_lane_chain_kernel): small windows,
-many single-segment streams, each lane walking its own stream's cut chain from the tile records
-and the group bounds.  Every cut list against the oracle (the reference's next_cut restated,
-oracle/gclmul_oracle.c), with the lane chain forced (RC_LANE_CHAIN=1) and, for comparison,
-disabled (the wave-per-stream spec kernel).  Runs on an MI355X only (-m gpu)."""
+"""GPU parity of the per-stream chains for small windows and many single-segment streams
+(kernels.hip rc_quad_chain_kernel: a quad of lanes per stream; rc_lane_chain_kernel: one lane),
+each walking its stream's cut chain from the tile records and the group bounds.  Every cut list
+against the oracle (the reference's next_cut restated, oracle/gclmul_oracle.c), with the quad
+chain forced (RC_LANE_CHAIN=1), the lane chain (=lane) and, for comparison, neither (=0: the
+wave-per-stream spec kernel).  Runs on an MI355X only (-m gpu)."""
 import random
 
 import numpy as np
@@ -48,7 +49,7 @@ PARAMS = [(2000, 80000), (500, 16384), (80000, 80000), (4, 4096 * 3), (12000, 13
           (64, 4096), (8, 3000)]
 
 
-@pytest.mark.parametrize('lane', ['1', '0'])
+@pytest.mark.parametrize('lane', ['1', 'lane', '0'])
 @pytest.mark.parametrize('mn,mx', PARAMS)
 @pytest.mark.parametrize('kind', ['random', 'zeros', 'periodic', 'sparse', 'splitmix'])
 def test_lane_chain_vs_oracle(monkeypatch, lane, mn, mx, kind):
