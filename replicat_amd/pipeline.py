@@ -13,8 +13,9 @@ What it replaces, in /root/reference/replicat/repository.py:
 The stream is gathered into host batches (``batch_bytes``, pinned) exactly as the batching shim
 does (replicat_amd/adapters.py): every batch but the last is chunked as an OPEN prefix (the
 reference's non-final ``next_cut`` calls), the last with its real framing, and the uncut tail
-is carried into the next batch.  Each batch is uploaded ONCE and everything runs on the bytes in
-HBM: the cut chain (rc_chunk_device), the chunk digests (rc_blake2b_chunks), the per-file
+is carried into the next batch.  Two batches are in flight: the files are read straight into
+one pinned batch (``readinto``) while the device works on the other, each batch on its own HIP
+stream.  Each batch is uploaded ONCE and everything runs on the bytes in HBM: the cut chain (rc_chunk_device), the chunk digests (rc_blake2b_chunks), the per-file
 incremental digests of small files (rc_blake2b_update_device: each file's bytes are fed once, in
 the batch that first holds them; a file's state lives in HBM across batches) and, with ``encryption``, every
 chunk's subkey (rc_blake2b_derive_chunks) and its AES-GCM encryption (rc_gcm_encrypt_chunks).
@@ -23,23 +24,26 @@ from the host batch, or the device's nonce || C || T when encrypted.
 
 The dedup table and the chunk -> file range map are host bookkeeping on a few integers per
 chunk, as in the reference.  Per-file digests of files of 1 MiB and more are hashed on host
-threads from the pinned batch while the device works (``file_digests='auto'``): a file digest is
+threads from the pinned batch, piece by piece as the pieces are read, while the device works
+(``file_digests='auto'``): a file digest is
 one sequential chain, which a host core advances ~10x faster than one device chain (measured,
 DESIGN.md §5c); ``file_digests='device'`` keeps every file on the device.  There is no CPU
 fallback: every cut, chunk digest, subkey and ciphertext comes from the HIP library, and a
 missing library raises.
 """
-import bisect
+import collections
+import io
 import os
+import threading
 import time
 from dataclasses import dataclass, field
-from typing import Dict, Iterator, List, Optional, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 
 from .chunker import MAX_LENGTH, MIN_LENGTH, GpuChunker, _current_device, normalize_params
-from .hashing import SLOT, STATE_BYTES, GpuBlake2b, state_init
-from .snapshot import ALIGNMENT, PIECE, sort_files
+from .hashing import SLOT, GpuBlake2b, state_init
+from .snapshot import PIECE, PieceReader, file_parts, sort_files
 
 # The device time of a batch has a floor: the BLAKE2b chain of its longest chunk (~55 ms for a
 # 5.12 MB chunk, DESIGN.md §3b), whatever the batch size; 1 GiB batches amortize it (256 MiB ones
@@ -90,48 +94,117 @@ class SnapshotStream:
     def snapshot_files(self):
         """The ``snapshot_files`` dict _chunk_done builds (repository.py:1374-1411): per file,
         its chunk parts ({'range', 'index', 'counter'}) and digest (metadata not collected)."""
-        starts = [(f.stream_start, i) for i, f in enumerate(self.files)]
         out = {}
-        for c in self.chunks:
-            point = bisect.bisect_left(starts, (c.stream_end + 1,))
-            for index in range(point - 1, -1, -1):
-                f = self.files[starts[index][1]]
-                if f.stream_end < c.stream_start:
-                    break
-                d = out.setdefault(f.path, {'path': f.path, 'chunks': [], 'digest': None})
-                d['chunks'].append({'range': [max(f.stream_start - c.stream_start, 0),
-                                              min(f.stream_end, c.stream_end) - c.stream_start],
-                                    'index': c.table_index, 'counter': c.counter})
-                if c.stream_end >= f.stream_end:
-                    d['digest'] = f.digest
+        for ci, fi, part in file_parts(self.files, self.chunks):
+            f, c = self.files[fi], self.chunks[ci]
+            d = out.setdefault(f.path, {'path': f.path, 'chunks': [], 'digest': None})
+            d['chunks'].append({'range': part, 'index': c.table_index, 'counter': c.counter})
+            if c.stream_end >= f.stream_end:
+                d['digest'] = f.digest
         return out
 
 
-def tagged_pieces(paths: Sequence[str], files: List[FileRecord], read=None
-                  ) -> Iterator[Tuple[bytes, int]]:
-    """repository.py:1413-1447's pieces for already-sorted paths, each with the number of files
-    known to be complete when it is yielded (data of file f: f; padding after file f: f + 1).
-    `files` receives a FileRecord when a file is opened; stream_end grows as it is read."""
-    pos = 0
-    prev = None
-    for path in paths:
-        if prev is not None:
-            pad = -(prev.stream_end - prev.stream_start) % ALIGNMENT
-            if pad:
-                pos += pad
-                yield bytes(pad), len(files)
-        f = FileRecord(path=str(path), stream_start=pos, stream_end=pos)
-        files.append(f)
-        prev = f
-        with (read(path) if read else open(path, 'rb')) as src:
+def _fstat_size(record, src):
+    try:
+        record.size = os.fstat(src.fileno()).st_size
+    except (AttributeError, OSError, ValueError, io.UnsupportedOperation):
+        record.size = None  # a read hook without a file descriptor
+
+
+class _Pending:
+    """Host digest pieces still to be hashed from one slot's bytes."""
+
+    def __init__(self):
+        self.n, self.err = 0, None
+        self.cv = threading.Condition()
+
+    def add(self):
+        with self.cv:
+            self.n += 1
+
+    def done(self, err=None):
+        with self.cv:
+            self.n -= 1
+            self.err = self.err or err
+            self.cv.notify_all()
+
+    def wait(self):
+        with self.cv:
+            while self.n:
+                self.cv.wait()
+            if self.err is not None:
+                raise self.err
+
+
+class _HostHash:
+    """A file digest on host threads: its pieces are hashed in order by one drain job at a time
+    (hashlib releases the GIL while it hashes), so files proceed in parallel and no pool thread
+    ever waits for another file's piece."""
+
+    def __init__(self, h):
+        self.h = h
+        self.q = collections.deque()
+        self.busy = False
+        self.lock = threading.Lock()
+
+    def push(self, view, pending, pool):
+        pending.add()
+        with self.lock:
+            self.q.append((view, pending))
+            if self.busy:
+                return
+            self.busy = True
+        pool.submit(self._drain)
+
+    def _drain(self):
+        while True:
+            with self.lock:
+                if not self.q:
+                    self.busy = False
+                    return
+                view, pending = self.q.popleft()
             try:
-                f.size = os.fstat(src.fileno()).st_size
-            except (AttributeError, OSError, ValueError):
-                f.size = None  # a read hook without a file descriptor
-            while piece := src.read(PIECE):
-                pos += len(piece)
-                f.stream_end += len(piece)
-                yield piece, len(files) - 1
+                self.h.update(view)
+            except BaseException as e:  # reported by the slot's wait
+                pending.done(e)
+            else:
+                pending.done()
+
+
+class _Slot:
+    """One batch in flight: its pinned host bytes, their device copy, the cut / digest outputs
+    and the HIP stream its work is queued on.  The batch's bytes sit at host[off:off + blen]:
+    the previous batch's uncut tail in the head room before `head`, the new pieces from `head`."""
+
+    def __init__(self, prod, torch):
+        dev = prod.dev
+        self.host = torch.empty(prod.capacity, dtype=torch.uint8, pin_memory=True)
+        self.hnp = self.host.numpy()
+        self.dbuf = torch.empty(prod.capacity, dtype=torch.uint8, device=dev)
+        self.d_cuts = torch.zeros(max(prod.cut_cap, 1), dtype=torch.int64, device=dev)
+        self.d_count = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.d_digests = torch.zeros((max(prod.cut_cap, 1), SLOT), dtype=torch.uint8, device=dev)
+        self.h_meta = torch.zeros(2, dtype=torch.int64, pin_memory=True)  # count, last cut end
+        self.stream = torch.cuda.Stream(device=dev)
+        self.ev_cut, self.ev_upd, self.ev_done = (torch.cuda.Event() for _ in range(3))
+        if prod.encryption is not None:
+            nb, total = prod.cipher.nonce_bytes, max(prod.cut_cap, 1)
+            self.d_keys = torch.zeros((total, SLOT), dtype=torch.uint8, device=dev)
+            self.h_nonces = torch.empty(total * nb, dtype=torch.uint8, pin_memory=True)
+            self.d_nonces = torch.empty(total * nb, dtype=torch.uint8, device=dev)
+            self.d_enc = torch.empty(max(prod.enc_cap, 1), dtype=torch.uint8, device=dev)
+            self.h_enc = torch.empty(max(prod.enc_cap, 1), dtype=torch.uint8, pin_memory=True)
+        self.reset(prod.head)
+
+    def reset(self, head):
+        self.off = head          # host offset of the batch's first byte
+        self.blen = 0            # bytes in the batch (carried tail + new pieces)
+        self.buf_start = 0       # stream offset of the batch's first byte
+        self.final = False
+        self.closed = 0          # files [0, closed) are complete within this batch
+        self.host_jobs = _Pending()  # host digest pieces reading this slot's bytes
+        self.items = []          # device file-digest items: (file index, final)
+        self.file_digests = None
 
 
 class DeviceSnapshotProducer:
@@ -151,7 +224,10 @@ class DeviceSnapshotProducer:
         self.device = int(device)
         self.dev = torch.device('cuda', self.device)
         self.chunker = GpuChunker(min_length, max_length, normalize_params(params), device=self.device)
+        # one hasher per kind of call: each makes one call per batch, so the two workspaces
+        # a handle alternates between (capi_digest.cpp) are never those of a batch in flight
         self.hasher = GpuBlake2b(length=digest_size, device=self.device)
+        self.file_hasher = GpuBlake2b(length=digest_size, device=self.device)
         self.min_length, self.max_length = min_length, max_length
         self.digest_size = digest_size
         self.batch_bytes = max(int(batch_bytes), 2 * max_length + 16)
@@ -160,31 +236,25 @@ class DeviceSnapshotProducer:
             raise ValueError(f'file_digests must be auto, device or host, not {file_digests!r}')
         self.file_digests = file_digests
         self._pool = None
-        # one batch plus the carried tail (< max_length) plus one piece of overshoot
-        self.capacity = self.batch_bytes + max_length + PIECE + 64
-        self.host = torch.empty(self.capacity, dtype=torch.uint8, pin_memory=True)
-        self.dbuf = torch.empty(self.capacity, dtype=torch.uint8, device=self.dev)
-        total, caps = self.chunker.capacity([self.capacity])
-        self.cut_cap = total
-        self.d_cuts = torch.zeros(max(total, 1), dtype=torch.int64, device=self.dev)
-        self.d_count = torch.zeros(1, dtype=torch.int64, device=self.dev)
-        self.d_digests = torch.zeros((max(total, 1), SLOT), dtype=torch.uint8, device=self.dev)
+        # head room for the carried tail (an OPEN batch leaves < max_length bytes uncut), one
+        # batch of new pieces, one piece of overshoot
+        self.head = (max_length + 127) // 64 * 64
+        self.capacity = self.head + self.batch_bytes + PIECE + 64
+        self.cut_cap, _ = self.chunker.capacity([self.capacity])
         self._init_state = np.frombuffer(state_init(digest_size), dtype=np.uint8)
         self.encryption = encryption
         if encryption is not None:
             from .cipher import GpuAesGcm
+            self.kdf_hasher = GpuBlake2b(length=digest_size, device=self.device)
             self.cipher = GpuAesGcm(key_bits=encryption.key_bits, nonce_bits=encryption.nonce_bits,
                                     device=self.device)
             kdf = state_init(self.cipher.key_bytes, key=encryption.shared_key,
                              salt=encryption.shared_kdf_params)
             self.d_kdf = torch.from_numpy(np.frombuffer(kdf, dtype=np.uint8).copy()).to(self.dev)
-            self.d_keys = torch.zeros((max(total, 1), SLOT), dtype=torch.uint8, device=self.dev)
-            nb = self.cipher.nonce_bytes
-            self.h_nonces = torch.empty(max(total, 1) * nb, dtype=torch.uint8, pin_memory=True)
-            self.d_nonces = torch.empty(max(total, 1) * nb, dtype=torch.uint8, device=self.dev)
-            out_total, _ = self.cipher.chunks_layout(self.chunker, [self.capacity])
-            self.d_enc = torch.empty(max(out_total, 1), dtype=torch.uint8, device=self.dev)
-            self.h_enc = torch.empty(max(out_total, 1), dtype=torch.uint8, pin_memory=True)
+            self.enc_cap, _ = self.cipher.chunks_layout(self.chunker, [self.capacity])
+        # two batches in flight: the host fills one while the device works on the other
+        self._slots = [_Slot(self, torch) for _ in range(2)]
+        self._look = bytearray(PIECE)  # the piece after a full batch (tells whether it is final)
 
     # ------------------------------------------------------------------- file digests
 
@@ -193,8 +263,8 @@ class DeviceSnapshotProducer:
     # lanes); a host core does ~1 GB/s.  Many small files hash in parallel on the
     # device within a batch, but a large file's chain would set the batch time (a 256 MiB file:
     # 2.9 s on the device, 0.27 s on a host core), so 'auto' hashes files of at least
-    # HOST_DIGEST_MIN bytes on host threads from the pinned batch, overlapped with the device
-    # work; 'device' and 'host' force one engine.
+    # HOST_DIGEST_MIN bytes on host threads, piece by piece as they are read, overlapped with
+    # the reads and the device work; 'device' and 'host' force one engine.
     HOST_DIGEST_MIN = 1 << 20
 
     def _on_host(self, fi, f, hstates, engine):
@@ -209,8 +279,14 @@ class DeviceSnapshotProducer:
                 engine[fi] = self.file_digests == 'host'
             if engine[fi]:
                 import hashlib
-                hstates[fi] = hashlib.blake2b(digest_size=self.digest_size)
+                hstates[fi] = _HostHash(hashlib.blake2b(digest_size=self.digest_size))
         return engine[fi]
+
+    def _collector(self):
+        if getattr(self, '_collect_pool', None) is None:
+            from concurrent.futures import ThreadPoolExecutor
+            self._collect_pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix='rc-collect')
+        return self._collect_pool
 
     def _host_pool(self):
         if self._pool is None:
@@ -222,157 +298,247 @@ class DeviceSnapshotProducer:
     # ------------------------------------------------------------------------------ run
 
     def run(self, paths: Sequence[os.PathLike], read=None) -> SnapshotStream:
+        """Batch k + 1 is read from the files while the device cuts and digests batch k, and
+        batch k's records are built while the device works on batch k + 1.  The uncut tail of
+        batch k (known once its cut chain is done, long before its digests) is copied to the
+        head of batch k + 1 on the host, so every batch is uploaded once."""
         import torch
-        stream = torch.cuda.current_stream(self.dev)
-        hs = stream.cuda_stream
         files: List[FileRecord] = []
-        chunks: List[ChunkRecord] = []
-        table: Dict[bytes, int] = {}
-        states = {}              # file index -> device state (open files only)
-        hstates = {}             # file index -> host hasher (open large files only)
-        engine = {}              # file index -> its digest runs on the host (decided once)
-        finalized = 0            # files [0, finalized) have their digest
-        hnp = self.host.numpy()
-        buf_start = 0            # stream offset of host[0]
-        blen = 0                 # bytes in the batch buffer
-        fed = 0                  # host[0:fed] already fed to the file digests
-        it = tagged_pieces(sort_files(paths), files, read)
-        nxt = next(it, None)
-        prof = self.profile = {'fill': 0.0, 'device': 0.0, 'host_digest_wait': 0.0, 'records': 0.0,
+        run = _Run(self, torch, files)
+        reader = PieceReader(sort_files(paths), files, read, record=FileRecord, on_open=_fstat_size)
+        # fill / wait_cut / enqueue / collect_join: this thread; collect_wait / records /
+        # host_digest_wait: the collector thread (overlapping the next fill)
+        prof = self.profile = {'fill': 0.0, 'wait_cut': 0.0, 'enqueue': 0.0, 'collect_join': 0.0,
+                               'collect_wait': 0.0, 'records': 0.0, 'host_digest_wait': 0.0,
                                'batches': 0}
         clock = time.perf_counter
-        while True:
-            t0 = clock()
-            prof['batches'] += 1
-            last_start = blen
-            while nxt is not None and (blen < self.batch_bytes or blen == 0):
-                piece, _ = nxt
-                last_start = blen
-                hnp[blen:blen + len(piece)] = np.frombuffer(piece, dtype=np.uint8)
-                blen += len(piece)
-                nxt = next(it, None)
-            final = nxt is None
-            closed = len(files) if final else nxt[1]
-            t1 = clock()
-            prof['fill'] += t1 - t0
-            # ---- host: per-file digests of the large files, hashed from the pinned batch while
-            # the device works on it (see _on_host)
-            lo_stream, hi_stream = buf_start + fed, buf_start + blen
-            host_jobs = []       # (file index, future or None, final)
-            for fi in range(finalized, len(files)):
-                if not self._on_host(fi, files[fi], hstates, engine):
-                    continue
-                f = files[fi]
-                a, b = max(f.stream_start, lo_stream), min(f.stream_end, hi_stream)
-                is_final = fi < closed
-                if b <= a and not is_final:
-                    continue
-                fut = None
-                if b > a:
-                    fut = self._host_pool().submit(hstates[fi].update,
-                                                   memoryview(hnp)[a - buf_start:b - buf_start])
-                host_jobs.append((fi, fut, is_final))
-            # ---- device: upload, cut chain, chunk digests
-            if blen:
-                self.dbuf[:blen].copy_(self.host[:blen], non_blocking=True)
-            ptr = self.dbuf.data_ptr()
-            self.chunker.chunk_device([ptr], [blen], [last_start], self.d_cuts.data_ptr(),
-                                      self.d_count.data_ptr(), hs, open_=not final)
-            self.hasher.digest_chunks(self.chunker, [ptr], [blen], self.d_cuts.data_ptr(),
-                                      self.d_count.data_ptr(), self.d_digests.data_ptr(), hs)
-            if self.encryption is not None:
+        prev, look, k = None, None, 0
+        # records are built on a collector thread (they copy chunk contents, holding the GIL)
+        # while this thread reads the next batch (the reads release it)
+        collected = [None, None]  # per slot: the collection of its last batch
+        collector = self._collector()
+        try:
+            look = reader.read_into(self._look)
+            while True:
+                s = self._slots[k & 1]
+                if collected[k & 1] is not None:  # the slot's previous batch is fully consumed
+                    t = clock()
+                    collected[k & 1].result()
+                    collected[k & 1] = None
+                    prof['collect_join'] += clock() - t
+                s.reset(self.head)
+                # ---- fill: the piece read ahead, then whole pieces up to batch_bytes of new bytes
+                t0 = clock()
+                n = last_rel = 0
+                while look is not None and (n < self.batch_bytes or n == 0):
+                    ln, _, fi = look
+                    at = self.head + n
+                    s.hnp[at:at + ln] = np.frombuffer(self._look, dtype=np.uint8, count=ln)
+                    run.host_piece(s, fi, at, ln)
+                    last_rel, n = n, n + ln
+                    # further pieces straight into the slot; the one after a full batch is
+                    # read ahead into _look
+                    while n < self.batch_bytes:
+                        got = reader.read_into(memoryview(s.hnp)[self.head + n:])
+                        if got is None:
+                            look = None
+                            break
+                        ln, _, fi = got
+                        run.host_piece(s, fi, self.head + n, ln)
+                        last_rel, n = n, n + ln
+                    else:
+                        look = reader.read_into(self._look)
+                        continue
+                    break
+                s.final = look is None
+                s.closed = len(files) if s.final else look[1]
+                new_lo = reader.pos - n - (look[0] if look is not None else 0)
+                t1 = clock()
+                prof['fill'] += t1 - t0
+                # ---- the previous batch's uncut tail to the head of this one
+                T, buf_start = 0, new_lo
+                if prev is not None:
+                    prev.ev_cut.synchronize()
+                    cnt, cut_end = int(prev.h_meta[0]), int(prev.h_meta[1])
+                    if cnt < 0:
+                        raise RuntimeError('cut capacity overflow')
+                    cut_end = cut_end if cnt else 0
+                    T = prev.blen - cut_end
+                    if T > self.head:
+                        raise RuntimeError(f'uncut tail of {T} bytes exceeds the head room')
+                    s.hnp[self.head - T:self.head] = prev.hnp[prev.off + cut_end:prev.off + prev.blen]
+                    buf_start = prev.buf_start + cut_end
+                t2 = clock()
+                prof['wait_cut'] += t2 - t1
+                s.off, s.blen, s.buf_start = self.head - T, T + n, buf_start
+                run.enqueue(s, prev, T, T + last_rel, new_lo, new_lo + n)
+                prof['batches'] += 1
+                prof['enqueue'] += clock() - t2
+                if prev is not None:
+                    collected[(k - 1) & 1] = collector.submit(run.collect, prev)
+                if s.final:
+                    collected[k & 1] = collector.submit(run.collect, s)
+                    for f in collected:
+                        if f is not None:
+                            f.result()
+                    break
+                prev = s
+                k += 1
+        finally:
+            reader.close()
+            for f in collected:
+                if f is not None:
+                    try:
+                        f.result()
+                    except BaseException:
+                        pass
+            for sl in self._slots:  # nothing of this run may still be queued or hashing
+                sl.stream.synchronize()
+                try:
+                    sl.host_jobs.wait()
+                except BaseException:
+                    pass
+        return SnapshotStream(files=files, chunks=run.chunks, chunks_table=run.table)
+
+
+class _Run:
+    """The bookkeeping of one DeviceSnapshotProducer.run: per-file digest states and engines,
+    the dedup table, the chunk records."""
+
+    def __init__(self, prod, torch, files):
+        self.p, self.torch, self.files = prod, torch, files
+        self.chunks: List[ChunkRecord] = []
+        self.table: Dict[bytes, int] = {}
+        self.states = {}     # file index -> device state (open device-engine files)
+        self.hstates = {}    # file index -> _HostHash (host-engine files)
+        self.engine = {}     # file index -> its digest runs on the host (decided once)
+        self.finalized = 0   # files [0, finalized) have their digest
+
+    def host_piece(self, s, fi, at, n):
+        """A file piece just placed at s.hnp[at:at + n]: hashed now on a host thread if the
+        file's digest is a host one."""
+        if fi is None or not self.p._on_host(fi, self.files[fi], self.hstates, self.engine):
+            return
+        self.hstates[fi].push(memoryview(s.hnp)[at:at + n], s.host_jobs, self.p._host_pool())
+
+    def enqueue(self, s, prev, T, last_start, new_lo, new_hi):
+        """Upload batch s and queue its cuts, chunk digests, subkeys + ciphertexts and the
+        device file digests of its new bytes on s.stream."""
+        torch, p = self.torch, self.p
+        hs = s.stream.cuda_stream
+        ptr = s.dbuf.data_ptr()
+        with torch.cuda.stream(s.stream):
+            if s.blen:
+                s.dbuf[:s.blen].copy_(s.host[s.off:s.off + s.blen], non_blocking=True)
+            p.chunker.chunk_device([ptr], [s.blen], [last_start], s.d_cuts.data_ptr(),
+                                   s.d_count.data_ptr(), hs, open_=not s.final)
+            # count and last cut end to pinned memory: the next batch's head needs them
+            s.h_meta[0:1].copy_(s.d_count, non_blocking=True)
+            last = torch.index_select(s.d_cuts, 0, (s.d_count - 1).clamp_(min=0))
+            s.h_meta[1:2].copy_(last, non_blocking=True)
+            s.ev_cut.record(s.stream)
+            p.hasher.digest_chunks(p.chunker, [ptr], [s.blen], s.d_cuts.data_ptr(),
+                                   s.d_count.data_ptr(), s.d_digests.data_ptr(), hs)
+            if p.encryption is not None:
                 # derive_shared_subkey(digest) and encrypt, per chunk, still in HBM; one
                 # os.urandom nonce per chunk as the adapter draws them (adapters.py:133)
-                self.hasher.derive_chunks(self.chunker, [blen], self.d_count.data_ptr(),
-                                          self.d_kdf.data_ptr(), self.d_digests.data_ptr(),
-                                          self.d_keys.data_ptr(), hs)
-                self.h_nonces.numpy()[:] = np.frombuffer(os.urandom(self.h_nonces.numel()),
-                                                         dtype=np.uint8)
-                self.d_nonces.copy_(self.h_nonces, non_blocking=True)
-                self.cipher.encrypt_chunks(self.chunker, [ptr], [blen], self.d_cuts.data_ptr(),
-                                           self.d_count.data_ptr(), self.d_keys.data_ptr(),
-                                           self.d_nonces.data_ptr(), self.d_enc.data_ptr(), hs)
-            # ---- device: per-file incremental digests over the fresh bytes [fed, blen)
-            items = []           # (file index, device ptr, length, final)
-            for fi in range(finalized, len(files)):
-                if engine.get(fi):
-                    continue
-                f = files[fi]
-                a, b = max(f.stream_start, lo_stream), min(f.stream_end, hi_stream)
+                p.kdf_hasher.derive_chunks(p.chunker, [s.blen], s.d_count.data_ptr(),
+                                           p.d_kdf.data_ptr(), s.d_digests.data_ptr(),
+                                           s.d_keys.data_ptr(), hs)
+                s.h_nonces.numpy()[:] = np.frombuffer(os.urandom(s.h_nonces.numel()),
+                                                      dtype=np.uint8)
+                s.d_nonces.copy_(s.h_nonces, non_blocking=True)
+                p.cipher.encrypt_chunks(p.chunker, [ptr], [s.blen], s.d_cuts.data_ptr(),
+                                        s.d_count.data_ptr(), s.d_keys.data_ptr(),
+                                        s.d_nonces.data_ptr(), s.d_enc.data_ptr(), hs)
+            # device file digests over the new bytes [T, blen): a file's state in HBM is
+            # advanced batch after batch, so this stream first waits for the previous batch's
+            # (files below prev.closed were closed by earlier batches, collected or not)
+            items = []
+            for fi in range(max(self.finalized, prev.closed if prev is not None else 0),
+                            len(self.files)):
+                f = self.files[fi]
+                a, b = max(f.stream_start, new_lo), min(f.stream_end, new_hi)
                 n = b - a if b > a else 0
-                is_final = fi < closed
+                is_final = fi < s.closed
                 if n == 0 and not is_final:
                     continue
-                items.append((fi, ptr + (a - buf_start) if n else 0, n, is_final))
-            file_digests = None
+                if p._on_host(fi, f, self.hstates, self.engine):
+                    continue
+                items.append((fi, ptr + T + (a - new_lo) if n else 0, n, is_final))
             if items:
+                if prev is not None:
+                    s.stream.wait_event(prev.ev_upd)
                 for fi, _, _, _ in items:
-                    if fi not in states:
-                        states[fi] = torch.from_numpy(self._init_state.copy()).to(self.dev)
-                scratch = torch.zeros((len(items), SLOT), dtype=torch.uint8, device=self.dev)
-                self.hasher.update_device([states[fi].data_ptr() for fi, _, _, _ in items],
-                                          [p for _, p, _, _ in items], [n for _, _, n, _ in items],
-                                          [1 if fin else 0 for _, _, _, fin in items],
-                                          scratch.data_ptr(), hs)
-                file_digests = scratch
-            # ---- results back
-            count = int(self.d_count.cpu()[0])
-            if count < 0:
-                raise RuntimeError('cut capacity overflow')
-            ends = self.d_cuts[:count].cpu().numpy().view(np.uint64).astype(np.int64)
-            digs = self.d_digests[:count, :self.digest_size].cpu().numpy()
-            enc = None
-            if self.encryption is not None:
-                over = self.cipher.nonce_bytes + 16
-                n_out = (int(ends[-1]) if count else 0) + count * over
-                self.h_enc[:n_out].copy_(self.d_enc[:n_out], non_blocking=True)
-                stream.synchronize()
-                enc = self.h_enc[:n_out].numpy()
-            if file_digests is not None:
-                fd = file_digests[:, :self.digest_size].cpu().numpy()
-                for j, (fi, _, _, fin) in enumerate(items):
-                    if fin:
-                        files[fi].digest = fd[j].tobytes()
-                        del states[fi]
-            t2 = clock()
-            prof['device'] += t2 - t1
-            for fi, fut, fin in host_jobs:  # before the batch buffer is reused
-                if fut is not None:
-                    fut.result()
+                    if fi not in self.states:
+                        self.states[fi] = torch.from_numpy(p._init_state.copy()).to(p.dev)
+                    else:
+                        self.states[fi].record_stream(s.stream)
+                scratch = torch.zeros((len(items), SLOT), dtype=torch.uint8, device=p.dev)
+                p.file_hasher.update_device([self.states[fi].data_ptr() for fi, _, _, _ in items],
+                                            [q for _, q, _, _ in items],
+                                            [n for _, _, n, _ in items],
+                                            [1 if fin else 0 for _, _, _, fin in items],
+                                            scratch.data_ptr(), hs)
+                s.file_digests = scratch
+                s.items = [(fi, fin) for fi, _, _, fin in items]
+            s.ev_upd.record(s.stream)
+            s.ev_done.record(s.stream)
+
+    def collect(self, s):
+        """Wait for batch s and turn it into records: cut ends, digests, dedup indices, contents
+        (sliced from the host batch, or the device's nonce || C || T), finished file digests."""
+        torch, p, prof, clock = self.torch, self.p, self.p.profile, time.perf_counter
+        t0 = clock()
+        s.ev_done.synchronize()
+        count = int(s.h_meta[0])
+        if count < 0:
+            raise RuntimeError('cut capacity overflow')
+        ends = s.d_cuts[:count].cpu().numpy().view(np.uint64).astype(np.int64)
+        digs = s.d_digests[:count, :p.digest_size].cpu().numpy()
+        enc = over = None
+        if p.encryption is not None:
+            over = p.cipher.nonce_bytes + 16
+            n_out = (int(ends[-1]) if count else 0) + count * over
+            with torch.cuda.stream(s.stream):
+                s.h_enc[:n_out].copy_(s.d_enc[:n_out], non_blocking=True)
+            s.stream.synchronize()
+            enc = s.h_enc[:n_out].numpy()
+        if s.file_digests is not None:
+            fd = s.file_digests[:, :p.digest_size].cpu().numpy()
+            for j, (fi, fin) in enumerate(s.items):
                 if fin:
-                    files[fi].digest = hstates.pop(fi).digest()
-            t3 = clock()
-            prof['host_digest_wait'] += t3 - t2
-            while finalized < closed and files[finalized].digest is not None:
-                finalized += 1
-            prev = 0
-            for k, e in enumerate(ends.tolist()):
-                d = digs[k].tobytes()
-                idx = table.get(d)
-                if idx is None:
-                    idx = table[d] = len(table)
-                if enc is not None:  # nonce || C || T of chunk k at prev + k (nonce_bytes + 16)
-                    o = prev + k * over
-                    contents = enc[o:o + (e - prev) + over].tobytes()
-                else:
-                    contents = hnp[prev:e].tobytes() if self.keep_contents else None
-                chunks.append(ChunkRecord(counter=len(chunks) + 1, stream_start=buf_start + prev,
-                                          stream_end=buf_start + e, digest=d, table_index=idx,
-                                          contents=contents))
-                prev = e
-            prof['records'] += clock() - t3
-            if final:
-                if prev != blen:
-                    raise RuntimeError(f'final batch left {blen - prev} bytes uncut')
-                break
-            # carry the uncut tail (< max_length bytes) to the front of the buffer
-            tail = blen - prev
-            if tail:
-                hnp[:tail] = hnp[prev:blen].copy()
-            buf_start += prev
-            blen = tail
-            fed = blen
-        return SnapshotStream(files=files, chunks=chunks, chunks_table=table)
+                    self.files[fi].digest = fd[j].tobytes()
+                    del self.states[fi]
+        t1 = clock()
+        prof['collect_wait'] += t1 - t0
+        chunks, table, hnp = self.chunks, self.table, s.hnp
+        prev = 0
+        for k, e in enumerate(ends.tolist()):
+            d = digs[k].tobytes()
+            idx = table.get(d)
+            if idx is None:
+                idx = table[d] = len(table)
+            if enc is not None:  # nonce || C || T of chunk k at prev + k (nonce_bytes + 16)
+                o = prev + k * over
+                contents = enc[o:o + (e - prev) + over].tobytes()
+            else:
+                contents = hnp[s.off + prev:s.off + e].tobytes() if p.keep_contents else None
+            chunks.append(ChunkRecord(counter=len(chunks) + 1, stream_start=s.buf_start + prev,
+                                      stream_end=s.buf_start + e, digest=d, table_index=idx,
+                                      contents=contents))
+            prev = e
+        t2 = clock()
+        prof['records'] += t2 - t1
+        s.host_jobs.wait()  # every host piece of this slot, before it is refilled
+        for fi in range(self.finalized, s.closed):
+            if self.engine.get(fi) and self.files[fi].digest is None:
+                self.files[fi].digest = self.hstates.pop(fi).h.digest()
+        prof['host_digest_wait'] += clock() - t2
+        while self.finalized < s.closed and self.files[self.finalized].digest is not None:
+            self.finalized += 1
+        if s.final and prev != s.blen:
+            raise RuntimeError(f'final batch left {s.blen - prev} bytes uncut')
 
 
 def snapshot_stream(paths, **kw) -> SnapshotStream:
@@ -381,4 +547,4 @@ def snapshot_stream(paths, **kw) -> SnapshotStream:
 
 
 __all__ = ['DeviceSnapshotProducer', 'SnapshotStream', 'FileRecord', 'ChunkRecord', 'ChunkEncryption',
-           'tagged_pieces', 'snapshot_stream', 'DEFAULT_BATCH']
+           'snapshot_stream', 'DEFAULT_BATCH']

@@ -10,9 +10,10 @@ Chunks straddle file boundaries and are mapped back to per-file byte ranges (:13
 files, parameters and key.
 """
 import bisect
+import io
 import os
 from dataclasses import dataclass, field
-from typing import Iterator, List, Optional, Sequence
+from typing import Iterator, List, Optional, Sequence, Tuple
 
 from .adapters import gclmulchunker
 
@@ -39,26 +40,88 @@ def sort_files(paths: Sequence[os.PathLike]) -> List[str]:
     return sorted((str(p) for p in paths), key=lambda p: (os.stat(p).st_size, p))
 
 
+class PieceReader:
+    """The pieces replicat's _stream_files yields (repository.py:1413-1447) for already-sorted
+    `paths`, read on demand into a caller's buffer: files in order, each in reads of at most
+    PIECE bytes (one ``read(PIECE)`` per piece, as the reference; a buffered file or BytesIO is
+    read straight into the buffer with ``readinto``, which returns the same bytes), and a zero
+    piece of (-len) % 4 bytes after every file that is followed by another.
+
+    `files` receives a record (``record(path=, stream_start=, stream_end=)``) when a file is
+    opened, and its stream_end grows as the file is read; `on_open(record, file_object)` runs
+    once per opened file.  Both stream_pieces and the device snapshot producer
+    (replicat_amd/pipeline.py) frame the stream through this one class."""
+
+    def __init__(self, paths: Sequence[str], files: Optional[list] = None, read=None,
+                 record=None, on_open=None):
+        self._paths = iter(paths)
+        self.files = files if files is not None else []
+        self._open = read if read else (lambda p: open(p, 'rb'))
+        self._record = record or SnapshotFile
+        self._on_open = on_open
+        self._cm = self._src = None
+        self._next = None   # the path after the current file (known before its padding)
+        self._pad = 0       # padding owed after the last closed file
+        self.pos = 0        # stream bytes so far
+
+    def read_into(self, dst) -> Optional[Tuple[int, int, Optional[int]]]:
+        """Place the next piece at the start of `dst` (writable, at least PIECE bytes).  Returns
+        (length, tag, file index) -- tag = the number of files known to be complete (data of
+        file f: f; padding after file f: f + 1), file index None for padding -- or None at the
+        end of the stream."""
+        mv = memoryview(dst).cast('B')
+        while True:
+            if self._src is not None:
+                n = self._read(mv)
+                if n:
+                    fi = len(self.files) - 1
+                    self.files[fi].stream_end += n
+                    self.pos += n
+                    return n, fi, fi
+                self.close()
+                f = self.files[-1]
+                self._pad = -(f.stream_end - f.stream_start) % ALIGNMENT
+            if self._next is None:
+                self._next = next(self._paths, None)
+                if self._next is None:
+                    return None
+            if self._pad:
+                pad, self._pad = self._pad, 0
+                mv[:pad] = bytes(pad)
+                self.pos += pad
+                return pad, len(self.files), None
+            path, self._next = self._next, None
+            f = self._record(path=str(path), stream_start=self.pos, stream_end=self.pos)
+            self.files.append(f)
+            self._cm = self._open(path)
+            self._src = self._cm.__enter__()
+            if self._on_open is not None:
+                self._on_open(f, self._src)
+
+    def _read(self, mv) -> int:
+        src = self._src
+        if isinstance(src, (io.BufferedReader, io.BytesIO)):
+            return src.readinto(mv[:PIECE]) or 0
+        piece = src.read(PIECE)
+        mv[:len(piece)] = piece
+        return len(piece)
+
+    def close(self):
+        cm, self._cm, self._src = self._cm, None, None
+        if cm is not None:
+            cm.__exit__(None, None, None)
+
+
 def stream_pieces(paths: Sequence[str], files_out: Optional[List[SnapshotFile]] = None,
                   read=None) -> Iterator[bytes]:
     """The pieces replicat's _stream_files yields for already-sorted `paths`."""
-    pos = 0
-    prev = None
-    for path in paths:
-        if prev is not None:
-            pad = -(prev.stream_end - prev.stream_start) % ALIGNMENT
-            if pad:
-                pos += pad
-                yield bytes(pad)
-        f = SnapshotFile(path=str(path), stream_start=pos, stream_end=pos)
-        if files_out is not None:
-            files_out.append(f)
-        prev = f
-        with (read(path) if read else open(path, 'rb')) as src:
-            while piece := src.read(PIECE):
-                pos += len(piece)
-                f.stream_end += len(piece)
-                yield piece
+    reader = PieceReader(paths, files_out, read)
+    buf = bytearray(PIECE)
+    try:
+        while (got := reader.read_into(buf)) is not None:
+            yield bytes(memoryview(buf)[:got[0]])
+    finally:
+        reader.close()
 
 
 def chunk_snapshot(paths: Sequence[os.PathLike], *, min_length: int = gclmulchunker.MIN_LENGTH,
@@ -75,17 +138,25 @@ def chunk_snapshot(paths: Sequence[os.PathLike], *, min_length: int = gclmulchun
     return files, chunks
 
 
-def file_ranges(files: Sequence[SnapshotFile], chunks: Sequence[SnapshotChunk]):
-    """Per file, the (chunk index, [part_start, part_end]) list -- repository.py:1374-1411."""
+def file_parts(files, chunks):
+    """(chunk index, file index, [part_start, part_end]) for every piece of a file inside a
+    chunk, in the order _chunk_done records them (repository.py:1374-1411): chunks in stream
+    order, the files a chunk touches from its last one backwards."""
     starts = [(f.stream_start, i) for i, f in enumerate(files)]
-    out = {f.path: [] for f in files}
     for ci, c in enumerate(chunks):
         point = bisect.bisect_left(starts, (c.stream_end + 1,))
         for index in range(point - 1, -1, -1):
-            f = files[starts[index][1]]
+            fi = starts[index][1]
+            f = files[fi]
             if f.stream_end < c.stream_start:
                 break
-            part_start = max(f.stream_start - c.stream_start, 0)
-            part_end = min(f.stream_end, c.stream_end) - c.stream_start
-            out[f.path].append((ci, [part_start, part_end]))
+            yield ci, fi, [max(f.stream_start - c.stream_start, 0),
+                           min(f.stream_end, c.stream_end) - c.stream_start]
+
+
+def file_ranges(files: Sequence[SnapshotFile], chunks: Sequence[SnapshotChunk]):
+    """Per file, the (chunk index, [part_start, part_end]) list -- repository.py:1374-1411."""
+    out = {f.path: [] for f in files}
+    for ci, fi, part in file_parts(files, chunks):
+        out[files[fi].path].append((ci, part))
     return out

@@ -21,7 +21,11 @@ import torch  # noqa: E402
 
 from oracle import oracle as o  # noqa: E402
 from replicat_amd import snapshot  # noqa: E402
-from replicat_amd.pipeline import ChunkEncryption, DeviceSnapshotProducer  # noqa: E402
+import importlib  # noqa: E402
+
+# RC_PRODUCER_MODULE: time another producer module (an A/B of two versions on one box)
+_mod = importlib.import_module(os.environ.get('RC_PRODUCER_MODULE', 'replicat_amd.pipeline'))
+ChunkEncryption, DeviceSnapshotProducer = _mod.ChunkEncryption, _mod.DeviceSnapshotProducer
 
 total_mib = int(sys.argv[1]) if len(sys.argv) > 1 else 256
 nfiles = int(sys.argv[2]) if len(sys.argv) > 2 else 1
@@ -80,6 +84,22 @@ def cpu_leg():
 
 
 dt, (ends, digs, fd) = timed(cpu_leg, reps=1)
+
+
+# the bound of the producer on few large files: each file digest is one sequential BLAKE2b
+# chain (repository.py:1437-1446), hashed here alone on one core from the page cache
+def file_digests_alone():
+    for p in paths:
+        with open(p, 'rb') as f:
+            h = hashlib.blake2b()
+            while piece := f.read(16 << 20):
+                h.update(piece)
+
+
+fdt, _ = timed(file_digests_alone)
+print(json.dumps({'variant': 'hashlib_file_digests_only', 'bytes': total, 's': round(fdt, 4),
+                  'gib_s': round(total / fdt / GIB, 3),
+                  'largest_file_s': round(fdt * max(sizes) / total, 4)}), flush=True)
 assert [c.stream_end for c in plain.chunks] == ends, 'cut mismatch'
 assert [c.digest for c in plain.chunks] == digs, 'digest mismatch'
 assert sorted(f.digest for f in plain.files) == sorted(fd), 'file digest mismatch'
