@@ -81,8 +81,10 @@ class Backend:
     def __init__(self, local_rank):
         import torch
         self.torch = torch
-        self.index = local_rank
-        torch.cuda.set_device(local_rank)
+        # one GPU per local rank; more ranks than GPUs (a rehearsal of the multi-rank path on a
+        # smaller box) share them round-robin
+        self.index = local_rank % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(self.index)
 
     def empty(self, nbytes):
         return self.torch.empty(nbytes, dtype=self.torch.uint8, device=self.device)
