@@ -253,6 +253,8 @@ uint64_t cut_cap_of(uint64_t min_length, uint64_t L) {
 int validate_streams(uint64_t n, const uint8_t *const *ptrs, const uint64_t *lens,
                      const uint64_t *last, bool device_aligned) {
     if (n && (!ptrs || !lens)) return fail(RC_ERR_ARGUMENT, "null stream arrays");
+    if (n >= (1ull << 31))  // tie markers carry the stream index in 31 bits (kernels.hip)
+        return fail(RC_ERR_ARGUMENT, "too many streams in one call: %llu", (unsigned long long)n);
     for (uint64_t i = 0; i < n; ++i) {
         const uint64_t P = last ? last[i] : 0;
         if (P > lens[i]) return fail(RC_ERR_ARGUMENT, "stream %llu: last piece start %llu > length %llu",

@@ -265,6 +265,7 @@ __device__ __forceinline__ void scan_records(const TileRecord *rec, uint64_t t_l
 struct TileRef {
     const uint8_t *base;
     uint64_t j0;
+    uint64_t s;  // its stream
     bool fast;
 };
 
@@ -279,7 +280,9 @@ __device__ __forceinline__ uint64_t tile_key_end(uint64_t j0, uint64_t L, uint64
 }
 
 constexpr uint32_t kLastLocal = 4 * kTileIters - 1;
-constexpr uint64_t kTieMark = ~0ull;  // TileRecord.j of a tile left to the exact path  // a lane's keys in a tile: 0 .. kLastLocal
+// TileRecord.j of a tile left to the exact path: ~stream index (its key: the candidate lanes;
+// streams are numbered below 2^31 here, checked by the host)
+constexpr uint64_t kTieMark = ~0ull;
 
 // Fast path over a tile whose kTileIters loads are in flight in x[].  As iteration `it` consumes
 // x[it] it re-issues x[it] for the wave's NEXT fast tile (if any), so every wave keeps
@@ -427,6 +430,7 @@ struct TileCursor {
         TileRef r;
         r.base = sload_ptr(d.ptr + s);
         r.j0 = (t - cur) * kTileKeys;
+        r.s = s;
         r.fast = __builtin_amdgcn_readfirstlane((uint32_t)tile_fast(r.j0, sload(d.len + s))) != 0;
         return r;
     }
@@ -538,7 +542,8 @@ __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restri
     // neighbour word, candidate words, one record store) so the compiler's in-order vmcnt
     // waits stay exact; the first store goes to the spare record at n_tiles.
     uint64_t pend_t = n_tiles, pend_j0 = 0;  // SGPRs: the pending tile and its first key
-    uint64_t pend_mask = 0;                   // candidate lanes (0 = marker record)
+    uint64_t pend_mask = 0;                   // candidate lanes
+    uint32_t pend_st = 0;                     // bit 31: a tie (marker record), low bits: stream
     uint32_t pend_lo = 0, pend_hi = 0, pend_jl = 0;  // per lane: candidate words and index
 
     for (;;) {
@@ -561,12 +566,15 @@ __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restri
 #ifndef RC_DIAG_NO_TAIL
         {
             const uint64_t k = full_key(tl, th, pend_lo, pend_hi);
-            uint64_t bk = 0, bj = kTieMark;
-            for (uint64_t m = pend_mask; m; m &= m - 1) {  // usually one lane
+            // a marker carries what the edge kernel needs: candidate lanes, ~stream
+            const bool ptie = pend_st >> 31;
+            const uint64_t pm = ptie ? 0 : pend_mask;
+            uint64_t bk = ptie ? pend_mask : 0, bj = kTieMark ^ (pend_st & 0x7fffffffu);
+            for (uint64_t m = pm; m; m &= m - 1) {  // usually one lane
                 const int l = __builtin_ctzll(m);
                 const uint64_t kl = lane_u64(k, l);
                 const uint64_t jl = pend_j0 + (uint32_t)__builtin_amdgcn_readlane(pend_jl, l);
-                if (bj == kTieMark || kl > bk || (kl == bk && jl < bj)) {
+                if (m == pm || kl > bk || (kl == bk && jl < bj)) {
                     bk = kl;
                     bj = jl;
                 }
@@ -591,7 +599,8 @@ __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restri
         n_ties += tie ? 1u : 0u;
         pend_t = t;
         pend_j0 = cur.j0;
-        pend_mask = tie ? 0 : cmask;
+        pend_mask = cmask;
+        pend_st = (tie ? 0x80000000u : 0u) | (uint32_t)cur.s;
         pend_jl = cand ? jl : win;  // non-candidates load the winner's (same) line
         const uint8_t *q = cur.base + 4 * (cur.j0 + pend_jl);
         pend_lo = ld_u32(q - (cur.j0 + pend_jl ? 4 : 0));  // never key 0; no read before the stream
@@ -606,12 +615,14 @@ __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restri
     }
     {
         const uint64_t k = full_key(tl, th, pend_lo, pend_hi);
-        uint64_t bk = 0, bj = kTieMark;
-        for (uint64_t m = pend_mask; m; m &= m - 1) {
+        const bool ptie = pend_st >> 31;
+        const uint64_t pm = ptie ? 0 : pend_mask;
+        uint64_t bk = ptie ? pend_mask : 0, bj = kTieMark ^ (pend_st & 0x7fffffffu);
+        for (uint64_t m = pm; m; m &= m - 1) {
             const int l = __builtin_ctzll(m);
             const uint64_t kl = lane_u64(k, l);
             const uint64_t jl = pend_j0 + (uint32_t)__builtin_amdgcn_readlane(pend_jl, l);
-            if (bj == kTieMark || kl > bk || (kl == bk && jl < bj)) {
+            if (m == pm || kl > bk || (kl == bk && jl < bj)) {
                 bk = kl;
                 bj = jl;
             }
@@ -650,6 +661,43 @@ __device__ __forceinline__ void exact_tile(const uint64_t *tl, const uint64_t *t
     }
 }
 
+// A tie tile of the fast path, from its marker: the first maximal exact key lies in one of the
+// candidate lanes (lanes whose top-16 maximum is the tile's, i.e. every key that can reach the
+// tile's maximum), so the wave evaluates those lanes' 64 keys each (edge lane i takes the
+// lane's key k = i & 3 of iteration i >> 2: local index 256 (i >> 2) + 4 c + (i & 3)), loads of
+// all (at most kTieLanes) candidates in flight together.  Key 0 of a stream does not exist.
+constexpr int kTieLanes = 4;
+__device__ __forceinline__ void exact_lanes(const uint64_t *tl, const uint64_t *th,
+                                            const StreamDesc &d, uint64_t s, uint64_t t,
+                                            uint64_t lanes, TileRecord *rec) {
+    const uint64_t j0 = (t - sload(d.tile_base + s)) * kTileKeys;
+    const uint8_t *base = sload_ptr(d.ptr + s);
+    const uint32_t i = lane_id();
+    const uint64_t local = (i >> 2) * 256 + (i & 3);
+    uint32_t lo[kTieLanes], hi[kTieLanes];
+    uint64_t jj[kTieLanes];
+    uint64_t m = lanes;
+#pragma unroll
+    for (int q = 0; q < kTieLanes; ++q) {
+        const uint32_t c = m ? (uint32_t)__builtin_ctzll(m) : 0u;
+        const uint64_t j = j0 + local + 4 * c;
+        const uint8_t *p = base + 4 * j;
+        lo[q] = ld_u32(j ? p - 4 : p);  // never a read before the stream
+        hi[q] = ld_u32(p);
+        jj[q] = (m && j) ? j : ~0ull;
+        m &= m - 1;
+    }
+    uint64_t bk = 0, bj = ~0ull;
+#pragma unroll
+    for (int q = 0; q < kTieLanes; ++q)
+        if (jj[q] != ~0ull) take_best(full_key(tl, th, lo[q], hi[q]), jj[q], bk, bj);
+    wave_best(bk, bj);
+    if (lane_id() == 0) {
+        rec[t].key = bk;
+        rec[t].j = bj;
+    }
+}
+
 // Exact tiles, one wave per item, grid-strided: items 0 .. n_waves - 1 are the tie lists of
 // the tile kernel's waves (xlist / xcount), the rest the host's list of tiles the fast path
 // does not take (tile_fast: the stream ends inside the tile; d.xtiles).  Each is recomputed
@@ -682,7 +730,12 @@ __global__ __launch_bounds__(256) void rc_edge_kernel(const KeyTables *__restric
             const uint32_t c = (uint32_t)__builtin_amdgcn_readfirstlane(xcount[e]);
             for (uint32_t i = 0; i < c; ++i) {
                 const uint64_t t = (uint32_t)__builtin_amdgcn_readfirstlane(xlist[t0 + i]);
-                exact_tile(tl, th, d, stream_of_tile(d, n_streams, t), t, rec, grp);
+                // the marker the tile kernel left: candidate lanes, ~stream
+                const uint64_t lanes = sload(&rec[t].key), s = ~sload(&rec[t].j) & 0x7fffffffu;
+                if (__builtin_popcountll(lanes) <= kTieLanes)
+                    exact_lanes(tl, th, d, s, t, lanes, rec);  // its group record stays valid
+                else  // e.g. constant data: every lane a candidate
+                    exact_tile(tl, th, d, s, t, rec, grp);
             }
         } else {
             const uint64_t t = sload(d.xtiles + 1 + (e - n_waves));

@@ -14,7 +14,7 @@ for r in $(seq ${ROUNDS:-3}); do
       if [ $v = old ]; then export RC_LIB_PATH=$B; else unset RC_LIB_PATH; fi
       timeout -k 10 300 python -u bench.py --config $cfg --steps 10 --warmup 2 --cpu-streams 0 --no-verify > $out/${v}_${cfg}_$r.log 2>&1 \
         || { echo "bench $v $cfg failed"; tail -n 5 $out/${v}_${cfg}_$r.log; exit 4; }
-      tail -n 1 $out/${v}_${cfg}_$r.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('$v', '$cfg', d['value'], d['ms_per_step'], r['kernel_ms'], r['chain_kernel_ms'])"
+      tail -n 1 $out/${v}_${cfg}_$r.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']; print('$v', '$cfg', d['value'], d['ms_per_step'], r['kernel_ms'], r['edge_kernel_ms'], r['chain_kernel_ms'])"
     done
   done
 done
