@@ -171,6 +171,36 @@ class _HostHash:
                 pending.done()
 
 
+def fill_batch(reader, look_buf, look, buf, head, batch_bytes, on_piece):
+    """Fill one batch at buf[head:] (a uint8 array): the piece read ahead (`look`, in
+    look_buf), then whole pieces straight from the files (PieceReader) while fewer than
+    batch_bytes new bytes are in place, then the next piece into look_buf: it tells whether the
+    batch is final and which files it closes.  on_piece(file index or None, offset, length)
+    follows every piece placed.  Returns (the next look, new bytes, offset of the last piece)."""
+    n = last_rel = 0
+    mv = memoryview(buf)
+    while look is not None and (n < batch_bytes or n == 0):
+        ln, _, fi = look
+        at = head + n
+        buf[at:at + ln] = np.frombuffer(look_buf, dtype=np.uint8, count=ln)
+        on_piece(fi, at, ln)
+        last_rel, n = n, n + ln
+        # further pieces straight into the batch; the one after a full batch into look_buf
+        while n < batch_bytes:
+            got = reader.read_into(mv[head + n:])
+            if got is None:
+                look = None
+                break
+            ln, _, fi = got
+            on_piece(fi, head + n, ln)
+            last_rel, n = n, n + ln
+        else:
+            look = reader.read_into(look_buf)
+            continue
+        break
+    return look, n, last_rel
+
+
 class _Slot:
     """One batch in flight: its pinned host bytes, their device copy, the cut / digest outputs
     and the HIP stream its work is queued on.  The batch's bytes sit at host[off:off + blen]:
@@ -329,27 +359,9 @@ class DeviceSnapshotProducer:
                 s.reset(self.head)
                 # ---- fill: the piece read ahead, then whole pieces up to batch_bytes of new bytes
                 t0 = clock()
-                n = last_rel = 0
-                while look is not None and (n < self.batch_bytes or n == 0):
-                    ln, _, fi = look
-                    at = self.head + n
-                    s.hnp[at:at + ln] = np.frombuffer(self._look, dtype=np.uint8, count=ln)
-                    run.host_piece(s, fi, at, ln)
-                    last_rel, n = n, n + ln
-                    # further pieces straight into the slot; the one after a full batch is
-                    # read ahead into _look
-                    while n < self.batch_bytes:
-                        got = reader.read_into(memoryview(s.hnp)[self.head + n:])
-                        if got is None:
-                            look = None
-                            break
-                        ln, _, fi = got
-                        run.host_piece(s, fi, self.head + n, ln)
-                        last_rel, n = n, n + ln
-                    else:
-                        look = reader.read_into(self._look)
-                        continue
-                    break
+                look, n, last_rel = fill_batch(reader, self._look, look, s.hnp, self.head,
+                                               self.batch_bytes,
+                                               lambda fi, at, ln: run.host_piece(s, fi, at, ln))
                 s.final = look is None
                 s.closed = len(files) if s.final else look[1]
                 new_lo = reader.pos - n - (look[0] if look is not None else 0)

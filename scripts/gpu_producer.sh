@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests/test_gpu_pipeline.py tests/test_snapshot.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread > $out/pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -n 3 $out/pytest.log
 [ $rc -eq 0 ] || exit $rc
-for args in "256 1" "4096 64"; do
+for args in ${PROBE_ARGS:-"256 1" "4096 64"}; do
   timeout -k 10 300 python -u scripts/producer_probe.py $args > "$out/probe_${args// /_}.log" 2>&1 || { echo "probe $args failed"; tail -20 "$out/probe_${args// /_}.log"; exit 3; }
   cat "$out/probe_${args// /_}.log" | grep -v amdgpu.ids
   if [ -f replicat_amd/_pipeline_r01.py ]; then

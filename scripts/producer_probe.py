@@ -60,7 +60,10 @@ def timed(fn, reps=3):
 
 
 enc = ChunkEncryption(shared_key=os.urandom(32), shared_kdf_params=os.urandom(16))
-for name, kw in (('plain', {}), ('encrypted', {'encryption': enc})):
+variants = [('plain', {}), ('encrypted', {'encryption': enc})]
+if 'parallel_reads' in DeviceSnapshotProducer.__init__.__code__.co_varnames:
+    variants.insert(1, ('plain_reads_in_line', {'parallel_reads': False}))
+for name, kw in variants:
     prod = DeviceSnapshotProducer(min_length=MIN, max_length=MAX, **kw)
     dt, res = timed(lambda: prod.run(paths))
     print(json.dumps({'variant': name, 'bytes': total, 'files': nfiles, 'chunks': len(res.chunks),

@@ -1,0 +1,71 @@
+"""CPU tests of the device producer's host side (replicat_amd/pipeline.py): the batches
+fill_batch places from the files (through snapshot.PieceReader) hold exactly the reference's
+stream (repository.py:1413-1447), whole pieces per batch, with the closed-file counts and file
+ranges the producer's digests rely on.  No GPU: fill_batch runs on a numpy buffer."""
+import os
+import random
+
+import numpy as np
+import pytest
+
+from replicat_amd import pipeline, snapshot
+
+
+def _fill_all(paths, batch):
+    files = []
+    reader = snapshot.PieceReader(paths, files, None, record=pipeline.FileRecord,
+                                  on_open=pipeline._fstat_size)
+    head = 64
+    buf = np.zeros(head + batch + snapshot.PIECE + 64, dtype=np.uint8)
+    look_buf = bytearray(snapshot.PIECE)
+    look = reader.read_into(look_buf)
+    batches, pieces = [], []
+    try:
+        while True:
+            look, n, last = pipeline.fill_batch(
+                reader, look_buf, look, buf, head, batch,
+                lambda fi, at, ln: pieces.append((fi, at - head, ln)))
+            batches.append((buf[head:head + n].tobytes(), last,
+                            len(files) if look is None else look[1]))
+            if look is None:
+                break
+    finally:
+        reader.close()
+    return batches, pieces, [(f.path, f.stream_start, f.stream_end, f.size) for f in files]
+
+
+def _files(tmp_path, seed, n=24):
+    rnd = random.Random(seed)
+    paths = []
+    for i in range(n):
+        size = rnd.choice([0, 1, 3, 4099, rnd.randrange(0, 3 << 20), rnd.randrange(0, 20 << 20)])
+        p = tmp_path / ('f%02d' % i)
+        p.write_bytes(os.urandom(size))
+        paths.append(p)
+    return snapshot.sort_files(paths)
+
+
+@pytest.mark.parametrize('batch', [1 << 20, 5 << 20, 64 << 20])
+def test_fill_batch_is_the_reference_stream(tmp_path, batch):
+    """Batches of whole pieces: concatenated, the reference's stream; every batch but the last
+    holds at least `batch` bytes and ends at a piece boundary; the closed-file count of a batch
+    is the number of files whose bytes all lie in it or before; the last piece's offset is where
+    the stream's final piece starts (P of the final batch)."""
+    paths = _files(tmp_path, batch)
+    batches, pieces, files = _fill_all(paths, batch)
+    pieces_ref = list(snapshot.stream_pieces(paths))
+    assert b''.join(b for b, _, _ in batches) == b''.join(pieces_ref)
+    assert [ln for _, _, ln in pieces] == [len(p) for p in pieces_ref]
+    pos = 0
+    for k, (data, last, closed) in enumerate(batches):
+        end = pos + len(data)
+        if k + 1 < len(batches):
+            assert len(data) >= batch
+        for fi, (_, a, b, _) in enumerate(files):
+            if fi < closed:  # complete: every byte in this batch or before
+                assert b <= end
+            else:  # still open: starts after this batch or runs past it
+                assert a >= end or b > end
+        pos = end
+    data, last, _ = batches[-1]
+    assert len(data) - last == len(pieces_ref[-1])
