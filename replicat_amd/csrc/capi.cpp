@@ -310,9 +310,12 @@ int stage_descriptors(rc_chunker *ch, Workspace &ws, uint64_t n, const uint8_t *
     std::copy(xt.begin(), xt.end(), u + 9 * n + 3);
     // Chain segments.  The chain of a stream is one wave walking ~(bound / chunk) steps; split
     // a stream only when the batch has too few streams to keep ~kChainWalkers waves busy, and
-    // never below 3 * max_length per segment (speculative chains must meet inside it).
+    // never below 3 * max_length per segment (speculative chains must meet inside it).  4096
+    // walkers (4 waves per SIMD): a walker is latency-bound, so shorter chains on more waves
+    // finish sooner even with the extension steps and the join (round 2, same box: config 2
+    // 0.19 -> 0.15 ms, 3 (ii) 0.31 -> 0.20, config 4 0.47 -> 0.24; 1024 walkers before).
     {
-        constexpr uint64_t kChainWalkers = 1024;
+        constexpr uint64_t kChainWalkers = 4096;
         uint64_t total = 0;
         for (uint64_t i = 0; i < n; ++i) {
             uint64_t b = 0;
