@@ -148,8 +148,10 @@ __device__ __forceinline__ void pf_addrs(uint32_t w, uint32_t lb_a, uint32_t lb_
     a[2] = __builtin_amdgcn_perm(w, lb_b, 0x0c020600u);
     a[3] = __builtin_amdgcn_perm(w, lb_b, 0x0c020700u) + 128;
 }
+// the four lookups of a word folded in two VALU: gfx950's v_bitop3_b32 (truth table 0x96) is a
+// three-input XOR (left to itself the compiler XORs them pairwise as the loads land)
 __device__ __forceinline__ uint32_t pf_gather(const uint32_t *a) {
-    return pf_lds(a[0]) ^ pf_lds(a[1]) ^ pf_lds(a[2]) ^ pf_lds(a[3]);
+    return __builtin_amdgcn_bitop3_b32(pf_lds(a[0]), pf_lds(a[1]), pf_lds(a[2]), 0x96) ^ pf_lds(a[3]);
 }
 
 // 32-bit prefilter entry of a word: top16(Lmap(w)) << 16 | top16(Hmap(w)).
