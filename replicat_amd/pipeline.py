@@ -312,6 +312,26 @@ class DeviceSnapshotProducer:
                 hstates[fi] = _HostHash(hashlib.blake2b(digest_size=self.digest_size))
         return engine[fi]
 
+    def close(self):
+        """Release the pinned batches, their device copies and the host threads (the object is
+        unusable afterwards; also on leaving a `with` block)."""
+        for pool in (self._pool, getattr(self, '_collect_pool', None)):
+            if pool is not None:
+                pool.shutdown(wait=True)
+        self._pool = self._collect_pool = None
+        self._slots = []
+        for h in ('chunker', 'hasher', 'file_hasher', 'kdf_hasher', 'cipher'):
+            obj = getattr(self, h, None)
+            if obj is not None and hasattr(obj, 'close'):
+                obj.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
+
     def _collector(self):
         if getattr(self, '_collect_pool', None) is None:
             from concurrent.futures import ThreadPoolExecutor
@@ -333,6 +353,8 @@ class DeviceSnapshotProducer:
         batch k (known once its cut chain is done, long before its digests) is copied to the
         head of batch k + 1 on the host, so every batch is uploaded once."""
         import torch
+        if not self._slots:
+            raise RuntimeError('DeviceSnapshotProducer is closed')
         files: List[FileRecord] = []
         run = _Run(self, torch, files)
         reader = PieceReader(sort_files(paths), files, read, record=FileRecord, on_open=_fstat_size)

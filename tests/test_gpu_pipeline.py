@@ -185,3 +185,14 @@ def test_read_hook_without_fileno(tmp_path):
     res = prod.run(paths, read=lambda p: io.BytesIO(files_data[os.path.basename(str(p))]))
     check_stream(res, files_data)
     assert all(f.size is None for f in res.files)
+
+
+def test_close_and_context_manager(tmp_path):
+    """close() (or leaving a with block) releases the batches, device handles and threads; a
+    closed producer refuses to run."""
+    files_data = {'a': random.Random(3).randbytes(300_000)}
+    paths = write(tmp_path, files_data)
+    with DeviceSnapshotProducer(min_length=2_000, max_length=80_000, batch_bytes=1 << 20) as prod:
+        check_stream(prod.run(paths), files_data)
+    with pytest.raises(RuntimeError, match='closed'):
+        prod.run(paths)
