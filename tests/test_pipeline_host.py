@@ -69,3 +69,43 @@ def test_fill_batch_is_the_reference_stream(tmp_path, batch):
         pos = end
     data, last, _ = batches[-1]
     assert len(data) - last == len(pieces_ref[-1])
+
+
+def test_host_file_digests_in_order_across_threads():
+    """_HostHash: pieces of many files pushed from one thread are hashed by a pool with one
+    drain job per file at a time -- each file's pieces in order, files in parallel -- and a
+    slot's _Pending waits for exactly its pieces (repository.py:1437-1446's per-file digests)."""
+    import hashlib
+    from concurrent.futures import ThreadPoolExecutor
+    rnd = random.Random(9)
+    datas = [rnd.randbytes(rnd.randrange(0, 3 << 20)) for _ in range(12)]
+    hs = [pipeline._HostHash(hashlib.blake2b()) for _ in datas]
+    slots = [pipeline._Pending() for _ in range(3)]
+    with ThreadPoolExecutor(4) as pool:
+        offs = [0] * len(datas)
+        k = 0
+        while any(o < len(d) for o, d in zip(offs, datas)):
+            for i, d in enumerate(datas):
+                if offs[i] < len(d):
+                    n = rnd.randrange(1, 200_000)
+                    hs[i].push(memoryview(d)[offs[i]:offs[i] + n], slots[k % 3], pool)
+                    offs[i] += n
+                    k += 1
+        for sl in slots:
+            sl.wait()
+            assert sl.n == 0
+    assert [h.h.digest() for h in hs] == [hashlib.blake2b(d).digest() for d in datas]
+
+
+def test_pending_reports_a_failed_piece():
+    from concurrent.futures import ThreadPoolExecutor
+
+    class Bad:
+        def update(self, view):
+            raise ValueError('boom')
+
+    sl = pipeline._Pending()
+    with ThreadPoolExecutor(2) as pool:
+        pipeline._HostHash(Bad()).push(memoryview(b'x'), sl, pool)
+        with pytest.raises(ValueError, match='boom'):
+            sl.wait()
