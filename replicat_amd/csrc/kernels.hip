@@ -407,10 +407,24 @@ __device__ __forceinline__ uint32_t wave_max_pk16(uint32_t v) {
     return pk_max_u16_s(pk_max_u16_s(r0, r1), pk_max_u16_s(r2, r3));
 }
 
-// Walks a wave's tile range across stream boundaries (all state wave-uniform).
+// Walks a wave's tile range across stream boundaries (all state wave-uniform).  kCache: the
+// stream's pointer and fast-tile count are loaded when the cursor enters it, not per tile (scalar
+// loads share lgkmcnt with the LDS reads, so each one in flight is a wait the next LDS use pays
+// for); off for rc_tile_kernel<4>, whose SGPRs would spill.
+template <bool kCache>
 struct TileCursor {
     StreamDesc d;
     uint64_t s, cur, next;
+    const uint8_t *base;
+    uint32_t nfast;  // the stream's tiles 0 .. nfast - 1 are on the fast path (tile_fast)
+    __device__ void enter() {
+        if constexpr (!kCache) return;
+        base = sload_ptr(d.ptr + s);
+        const uint64_t L = sload(d.len + s);
+        // tile_fast(j0, L) for j0 = i * kTileKeys  <=>  i < nfast
+        nfast = L >= 8 && (L - 4) / 4 >= kTileKeys - 1
+                    ? (uint32_t)(((L - 4) / 4 - (kTileKeys - 1)) / kTileKeys + 1) : 0u;
+    }
     __device__ void init(const StreamDesc &dd, uint64_t n_streams, uint64_t t) {
         d = dd;
         uint64_t lo = 0, hi = n_streams;  // largest s with tile_base[s] <= t
@@ -422,18 +436,27 @@ struct TileCursor {
         s = lo;
         cur = sload(d.tile_base + s);
         next = sload(d.tile_base + s + 1);
+        enter();
     }
     __device__ TileRef at(uint64_t t) {  // t must not decrease between calls
-        while (t >= next) {
-            ++s;
-            cur = next;
-            next = sload(d.tile_base + s + 1);
+        if (t >= next) {
+            do {
+                ++s;
+                cur = next;
+                next = sload(d.tile_base + s + 1);
+            } while (t >= next);
+            enter();
         }
         TileRef r;
-        r.base = sload_ptr(d.ptr + s);
         r.j0 = (t - cur) * kTileKeys;
         r.s = s;
-        r.fast = __builtin_amdgcn_readfirstlane((uint32_t)tile_fast(r.j0, sload(d.len + s))) != 0;
+        if constexpr (kCache) {
+            r.base = base;
+            r.fast = t - cur < nfast;
+        } else {
+            r.base = sload_ptr(d.ptr + s);
+            r.fast = __builtin_amdgcn_readfirstlane((uint32_t)tile_fast(r.j0, sload(d.len + s))) != 0;
+        }
         return r;
     }
 };
@@ -519,7 +542,7 @@ __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restri
         return;
     }
 
-    TileCursor cursor;
+    TileCursor<G == 1> cursor;
     cursor.init(d, n_streams, t);
     TileRef cur = cursor.at(t);
     while (!cur.fast && ++t < t_end) cur = cursor.at(t);
