@@ -1,0 +1,57 @@
+"""CPU tests of bench.py's measurement bookkeeping (SURVEY.md §8 d): the roofline's two bases,
+its nulls, and the PMC traffic that may only come from a summary of the same library build."""
+import json
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+GB = 1e9
+
+
+def test_roofline_two_bases():
+    L, read = 68_719_476_736, 63_476_596_736
+    r = bench.roofline(L, read, 10.0, 0.02, 0.15, 64.5 * GB, 'x', 'id')
+    assert r['achieved'] == pytest.approx(L / 10e-3 / GB, abs=0.1)
+    assert r['frac'] == pytest.approx(L / 10e-3 / GB / bench.HBM_PEAK_GBS, abs=1e-4)
+    assert r['frac_read'] == pytest.approx(read / 10e-3 / GB / bench.HBM_PEAK_GBS, abs=1e-4)
+    assert r['frac_read'] < r['frac'] <= 1.0
+    assert r['traffic'] == round(64.5 * GB) and r['bound'] == 'hbm'
+
+
+def test_roofline_null_when_nothing_is_read():
+    """config 3 (i): every stream cut by the tail rule alone -- no roofline, not a 1000x frac."""
+    r = bench.roofline(68_719_476_736, 0, 0.005, 0.005, 0.12, None, 'x', 'id')
+    assert r['achieved'] is None and r['frac'] is None and r['frac_read'] is None
+    assert 'tail rule' in r['note']
+
+
+def test_roofline_null_above_peak():
+    r = bench.roofline(10 * GB, 10 * GB, 1.0, 0.0, 0.0, None, 'x', 'id')  # 10 TB/s
+    assert r['frac'] is None and r['note'] == 'not a measurement'
+
+
+def test_pmc_traffic_same_build_only(tmp_path, monkeypatch):
+    d = tmp_path / 'profiles' / 'r09'
+    d.mkdir(parents=True)
+    (d / 'pmc_summary.json').write_text(json.dumps({
+        'workload': 'config2', 'build_id': 'aaaa',
+        'rc_tile_kernel': {'hbm_read_bytes_corrected': 64e9, 'hbm_write_bytes': 1e8}}))
+    monkeypatch.setattr(bench, 'ROOT', str(tmp_path))
+    got, src = bench.pmc_traffic('2', 1024, 64 << 20, 'aaaa')
+    assert got == pytest.approx(64.1e9) and src.endswith('pmc_summary.json')
+    got, why = bench.pmc_traffic('2', 1024, 64 << 20, 'bbbb')
+    assert got is None and 'aaaa' in why and 'bbbb' in why
+    assert bench.pmc_traffic('4', 16, 8 << 30, 'aaaa')[0] is None
+
+
+def test_cpu_share_caps_at_the_box_share(monkeypatch):
+    monkeypatch.setattr(os, 'sched_getaffinity', lambda pid: set(range(256)))
+    monkeypatch.setenv('OMP_NUM_THREADS', '16')
+    assert bench.cpu_share() == (16, 256)
+    monkeypatch.delenv('OMP_NUM_THREADS')
+    assert bench.cpu_share() == (256, 256)
