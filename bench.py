@@ -9,11 +9,19 @@ every needed byte + chain kernel per stream), cut offsets left in HBM.
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3i|3ii|3iii|4|5|harness]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (N > 1)
 
+`--gpus N` with N > 1 and no launcher around it (WORLD_SIZE unset) starts the N ranks itself:
+a child `python -m torch.distributed.run --nproc-per-node N` over this same script, before
+anything touches the GPU; bench.py exits with the child's status.  Every rank checks that the
+world size equals --gpus and that the ranks hold N DISTINCT devices (PCI bus id / UUID
+gathered into the line); ranks sharing a device exit non-zero unless --share-gpus is given (a
+one-GPU rehearsal), and then the roofline is null (the ranks' HIP events time each other).
+
 Ranks shard the work per stream (config 2: stream ids rank*1024 ..; config 4: stream i on
 GPU i mod 8) with no data-path collective: "scaling": "weak".  The process group is gloo and
 carries only the barriers, the max-over-ranks time and the parity flags -- never stream data.
 Rank 0 prints one JSON line.  Parity is checked in-run against the reference's cut-list
-digests (tests/golden: config 2, 3 (ii), 3 (iii), 4 on every rank, 5, harness).
+digests (tests/golden: config 2 (key ff, and the seeded key's first 128 streams), 3 (i),
+3 (ii), 3 (iii), 4 on every rank, 5, harness).
 
 `--config harness` is the reference's own benchmark (Repository._benchmark_chunker,
 /root/reference/replicat/repository.py:1984-2008): 10 x 512,000,000 Random(0) bytes as one
@@ -67,7 +75,54 @@ def parse(argv=None):
                    help='CPU-baseline processes (default: the cores this process may use)')
     p.add_argument('--e2e', action='store_true', help='also time the host-resident path')
     p.add_argument('--no-verify', action='store_true')
+    p.add_argument('--share-gpus', action='store_true',
+                   help='allow ranks to share a device (a rehearsal of the N-rank path on a '
+                        'smaller box; the line then carries no roofline)')
     return p.parse_args(argv)
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args, argv, script=None):
+    """Run the N ranks of `--gpus N` as one child `torch.distributed.run` over this script
+    (one process per GPU; the driver's own N > 1 command has the same shape).  Nothing here
+    touches the GPU -- the children initialise their devices themselves -- and the parent
+    waits for the child instead of replacing itself.  Returns the child's exit status."""
+    import subprocess
+    script = os.path.abspath(script or sys.argv[0])
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
+           f'--nproc-per-node={args.gpus}', '--master-addr', '127.0.0.1',
+           '--master-port', str(_free_port()), script] + list(argv)
+    env = dict(os.environ)
+    env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
+    return subprocess.call(cmd, env=env)
+
+
+def cli(argv=None, backend=None, script=None):
+    """The command line: N > 1 without a launcher starts the ranks; otherwise this process is
+    one rank (or the only one).  Returns an exit status."""
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse(argv)
+    if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        return launch_ranks(args, argv, script)
+    try:
+        main(argv, backend=backend or Backend)
+    except RankMismatch as e:
+        print(f'bench.py: {e}', file=sys.stderr, flush=True)
+        return 3
+    return 0
+
+
+class RankMismatch(RuntimeError):
+    """The ranks do not match the request: world size != --gpus, or ranks sharing a device
+    without --share-gpus."""
 
 
 # ------------------------------------------------------------------ device plumbing
@@ -81,10 +136,19 @@ class Backend:
     def __init__(self, local_rank):
         import torch
         self.torch = torch
-        # one GPU per local rank; more ranks than GPUs (a rehearsal of the multi-rank path on a
-        # smaller box) share them round-robin
+        # one GPU per local rank; with fewer visible devices than ranks they wrap round, and
+        # main() refuses that (distinct physical devices checked) unless --share-gpus
         self.index = local_rank % max(1, torch.cuda.device_count())
         torch.cuda.set_device(self.index)
+
+    def identity(self):
+        """The physical device this rank runs on: ordinal, PCI location, UUID, name."""
+        p = self.torch.cuda.get_device_properties(self.index)
+        pci = '%04x:%02x:%02x' % (getattr(p, 'pci_domain_id', 0), getattr(p, 'pci_bus_id', 0),
+                                  getattr(p, 'pci_device_id', 0))
+        return {'device': self.index, 'pci': pci, 'uuid': str(getattr(p, 'uuid', '')),
+                'name': p.name, 'visible': os.environ.get('HIP_VISIBLE_DEVICES')
+                or os.environ.get('ROCR_VISIBLE_DEVICES') or os.environ.get('CUDA_VISIBLE_DEVICES')}
 
     def empty(self, nbytes):
         return self.torch.empty(nbytes, dtype=self.torch.uint8, device=self.device)
@@ -175,15 +239,6 @@ def shard_ids(config, rank, n):
     if config == '4':
         return [rank + 8 * i for i in range(n)]
     return [rank * n + i for i in range(n)]
-
-
-def reduce_max(values, dist, device):
-    """Max over ranks of a few floats through an initialised process group (kept for callers
-    that hold their own group; main() uses Ranks.max)."""
-    import torch
-    t = torch.tensor(values, dtype=torch.float64, device=device)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return t.tolist()
 
 
 def cut_digest(cuts_dev, counts_dev, caps):
@@ -557,6 +612,14 @@ def check_parity(args, n, size, rank, long, edit, ends, digest):
     ff = args.key == 'ff'
     if args.config == '2' and ff and n == 1024 and size == 64 << 20 and rank == 0:
         return digest == gold['config2_ff']['sha256'], 'rank 0 (streams 0..1023)'
+    if args.config == '2' and not ff and n >= 128 and size == 64 << 20 and rank == 0:
+        # an encrypted repository's key (repository.py:174-181): the reference cut the first
+        # 128 streams with synth.seeded_key(1) (tests/golden/make_golden.py)
+        g = gold['config2_seeded_first128']
+        from replicat_amd import synth
+        assert synth.seeded_key(1).hex() == g['params']
+        return (G.cutlist_digest(ends[:128]) == g['sha256'],
+                'rank 0, seeded key: streams 0..127')
     if args.config == '3iii' and ff and rank == 0 and n == 65536:
         return digest == gold['config3iii']['sha256'], 'all 65536 streams'
     if args.config == '3iii' and ff and rank == 0 and n >= 4096:
@@ -615,11 +678,29 @@ def roofline(bytes_per_step, read, tile_avg, edge_avg, chain_avg, traffic, traff
 LAST = {}  # the last main() call's cut lists, device and parity (tests/test_bench_ranks.py)
 
 
+def check_ranks(args, ranks, be):
+    """Each rank's device, gathered; RankMismatch (every rank raises it alike) when the world
+    is not --gpus ranks or, without --share-gpus, when two ranks hold the same device.
+    Returns (identities, shared)."""
+    if ranks.world != args.gpus:
+        ranks.close()
+        raise RankMismatch(f'{ranks.world} rank(s) running but --gpus {args.gpus} requested')
+    ids = ranks.gather(dict(be.identity(), rank=ranks.rank))
+    keys = [i.get('uuid') or i.get('pci') for i in ids]
+    shared = len(set(keys)) < len(keys)
+    if shared and not args.share_gpus:
+        ranks.close()
+        raise RankMismatch(f'{len(keys)} ranks on {len(set(keys))} distinct device(s) '
+                           f'({", ".join(i["pci"] for i in ids)}); --share-gpus to rehearse')
+    return ids, shared
+
+
 def main(argv=None, backend=Backend):
     args = parse(argv)
     ranks = Ranks()
     world, rank = ranks.world, ranks.rank
     be = backend(ranks.local)
+    devices, shared = check_ranks(args, ranks, be)
 
     from replicat_amd import synth
     key = b'\xff' * 16 if args.key == 'ff' else synth.seeded_key(1)
@@ -697,6 +778,8 @@ def main(argv=None, backend=Backend):
     elapsed = time.perf_counter() - t0
     ch.timing(False)
     tile_ms, edge_ms, chain_ms, calls = ch.read_kernel_timing()
+    mine = {'rank': rank, 'elapsed_s': round(elapsed, 6),
+            'tile_kernel_ms': round(tile_ms / max(calls, 1), 3)}
     elapsed, tile_ms, edge_ms, chain_ms = ranks.max([elapsed, tile_ms, edge_ms, chain_ms])
 
     bytes_per_step = sum(lens) if long is None else long.L // world
@@ -715,10 +798,14 @@ def main(argv=None, backend=Backend):
         if not custom:
             parity, scope = check_parity(args, n, size, rank, long, edit, ends, digest)
     LAST.update(device=be.index, ends=ends, parity=parity, rank=rank)
-    flags = ranks.gather(parity)
+    mine['parity'] = parity
+    per_rank = ranks.gather(mine)
+    flags = [r['parity'] for r in per_rank]
     if args.config == '4' and all(f is not None for f in flags):
         parity = all(flags)  # every rank checked its own shard
         scope = f'{len(flags)} rank(s), each its own 16 streams'
+    for r, d in zip(per_rank, devices):
+        r.update(device=d['device'], pci=d['pci'], uuid=d['uuid'])
 
     result = None
     if rank == 0:
@@ -728,8 +815,15 @@ def main(argv=None, backend=Backend):
             else (None, 'seeded key: no PMC summary')
         roof = roofline(bytes_per_step, bytes_needed(max_len, lens, last), tile_ms / calls,
                         edge_ms / calls, chain_ms / calls, traffic, traffic_src, bid)
+        if shared:
+            # ranks on one device: each rank's HIP events also time the other ranks' kernels
+            roof.update(achieved=None, frac=None, achieved_read=None, frac_read=None,
+                        note='ranks share a device (--share-gpus): kernel times overlap, '
+                             'no roofline')
         cpu = None
-        if world == 1 and args.key == 'ff' and args.config == '2' and args.cpu_streams != 0:
+        # the CPU leg runs on rank 0 after the timed region, at every N (the other ranks wait
+        # at the final barrier); its sample is rank 0's own streams
+        if args.key == 'ff' and args.config == '2' and args.cpu_streams != 0:
             procs, seen = cpu_share()
             procs = args.cpu_procs or procs
             sample = min(args.cpu_streams or n, n)
@@ -738,7 +832,7 @@ def main(argv=None, backend=Backend):
             if ends is not None:
                 cpu['matches_gpu'] = bool(all(np.array_equal(np.asarray(cpu_ends[i], np.uint64),
                                                              ends[i]) for i in cpu_ends))
-        elif harness is not None and args.cpu_streams != 0 and world == 1:
+        elif harness is not None and args.cpu_streams != 0:
             cpu, lengths = harness_cpu(harness, min_len, max_len)
             if cpu is not None and ends is not None:
                 cpu['matches_gpu'] = bool(np.array_equal(np.cumsum(lengths).astype(np.uint64),
@@ -765,6 +859,11 @@ def main(argv=None, backend=Backend):
             'cpu_baseline': cpu,
             'parity_sha256': parity,
             'parity_scope': scope,
+            'devices': [d['pci'] for d in devices],
+            'distinct_devices': len({d['uuid'] or d['pci'] for d in devices}),
+            'ranks_seen': world,
+            'shared_devices': shared,
+            'per_rank': per_rank,
         }
         if harness is not None:
             result['rate_GBps'] = round(bytes_per_step * args.steps / elapsed / 1e9, 3)
@@ -817,4 +916,4 @@ def e2e_rates(ch, n, size):
 
 
 if __name__ == '__main__':
-    main()
+    sys.exit(cli())

@@ -47,7 +47,7 @@ extern "C" {
 
 typedef struct rc_chunker rc_chunker;
 
-/* Library / ABI version, e.g. 200 = 0.2.0. */
+/* Library / ABI version: 300 = 0.3.0 (replicat_amd.__version__; tests/test_cabi.py checks they agree). */
 int rc_version(void);
 
 /* Build id: a hash over the library's sources and compile flags, set by replicat_amd/build.py

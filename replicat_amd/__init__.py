@@ -7,4 +7,4 @@ hand-written gfx950 HIP kernels in ``libreplicat_chunker.so`` behind a C ABI
 ``_replicat_adapters`` surface (``replicat_amd._replicat_adapters``) and adds a batch API over
 many device- or host-resident streams (``replicat_amd.chunker``).
 """
-__version__ = '0.1.0'
+__version__ = '0.3.0'

@@ -69,16 +69,10 @@ class gclmulchunker(ChunkerAdapter):
         return self._gpu
 
     def close(self):
-        """Release the device chunker (tables, workspaces, pinned staging)."""
-        gpu, self._gpu, self._key = self._gpu, None, None
-        if gpu is not None:
-            gpu.close()
-
-    def __del__(self):
-        try:
-            self.close()
-        except Exception:
-            pass
+        """Drop this adapter's device chunker (tables, workspaces, pinned staging).  It is
+        released with its last reference (GpuChunker.__del__), not here: a generator of an
+        earlier __call__ may still be cutting with it, and must be able to finish."""
+        self._gpu, self._key = None, None
 
     def __call__(self, chunk_iterator: Iterator[ByteString], *,
                  params: Optional[bytes] = None) -> Iterator[bytes]:

@@ -36,14 +36,32 @@ def hipcc():
     raise RuntimeError('hipcc not found (ROCm 7.x required)')
 
 
+_COMPILER = {}
+
+
+def compiler_id():
+    """The resolved hipcc and its version banner (a ROCm upgrade changes the code object)."""
+    if 'id' not in _COMPILER:
+        cc = hipcc()
+        try:
+            banner = subprocess.run([cc, '--version'], capture_output=True, text=True,
+                                    timeout=120).stdout
+        except (OSError, subprocess.SubprocessError):
+            banner = ''
+        _COMPILER['id'] = os.path.realpath(cc) + '\n' + banner.strip()
+    return _COMPILER['id']
+
+
 def source_id(extra=()):
-    """Hash of every source/header (path relative to the package) and the compile flags."""
+    """Hash of every source/header (path relative to the package), the compile flags and the
+    compiler (path + version)."""
     h = hashlib.sha256()
     for p in SOURCES + HEADERS:
         h.update(os.path.relpath(p, ROOT).encode() + b'\0')
         with open(p, 'rb') as f:
             h.update(f.read())
     h.update(' '.join(FLAGS + list(extra)).encode())
+    h.update(b'\0' + compiler_id().encode())
     return h.hexdigest()[:16]
 
 

@@ -475,7 +475,7 @@ ChainParams chain_params(const rc_chunker *ch, const Plan &plan, uint64_t max_st
 
 extern "C" {
 
-int rc_version(void) { return 200; }
+int rc_version(void) { return 300; }
 
 #ifndef RC_BUILD_ID
 #define RC_BUILD_ID "unknown"

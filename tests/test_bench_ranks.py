@@ -3,7 +3,6 @@ GPU box too -- the data path has no collective), with the device calls replaced 
 stand-in whose chunker is the oracle.  Checks device selection per LOCAL_RANK, the shards each
 rank fills and chunks, the weak-scaling value formula, the max-over-ranks timing, per-rank
 parity gathering, and config 3 (ii)'s split + gather + splice of one stream over two ranks."""
-import ctypes
 import os
 import socket
 
@@ -13,88 +12,9 @@ import torch
 import torch.multiprocessing as mp
 
 import bench
+from bench_standin import CpuBackend
 
 GIB = 1 << 30
-
-
-class OracleChunker:
-    """GpuChunker's surface as bench.py uses it, over host memory, computed by the oracle."""
-
-    def __init__(self, min_length, max_length, key, log):
-        from oracle import oracle as o
-        self.o, self.log = o, log
-        self.min_length, self.max_length, self.key = min_length, max_length, key
-        self.calls = 0
-
-    def capacity(self, lens):
-        step = max(4, (self.min_length + 3) & ~3)
-        caps = np.array([int(L) // step + 3 for L in lens], dtype=np.uint64)
-        return int(caps.sum()), caps
-
-    def chunk_device(self, ptrs, lens, last, cuts_ptr, counts_ptr, stream=0, open_=False):
-        _, caps = self.capacity(lens)
-        base = np.concatenate([[0], np.cumsum(caps)[:-1]]).astype(np.int64)
-        n = len(lens)
-        cuts = np.ctypeslib.as_array((ctypes.c_uint64 * int(caps.sum())).from_address(cuts_ptr))
-        counts = np.ctypeslib.as_array((ctypes.c_int64 * n).from_address(counts_ptr))
-        for i, (p, L) in enumerate(zip(ptrs, lens)):
-            data = np.frombuffer(ctypes.string_at(int(p), int(L)), dtype=np.uint8)
-            P = int(L) if open_ else (int(last[i]) if last is not None else 0)
-            ends = self.o.chunk_stream(data, self.min_length, self.max_length, self.key, P)
-            if open_:  # non-final prefix: cut while L - s >= max (RC_OPEN)
-                out, s = [], 0
-                for e in ends:
-                    if L - s < self.max_length:
-                        break
-                    out.append(e)
-                    s = e
-                ends = out
-            cuts[base[i]:base[i] + len(ends)] = ends
-            counts[i] = len(ends)
-            self.log.append(bytes(data[:16]))
-        self.calls += 1
-
-    def timing(self, enable):
-        if enable:
-            self.calls = 0
-
-    def read_kernel_timing(self):
-        return 1.0 * self.calls, 0.1 * self.calls, 0.2 * self.calls, self.calls
-
-
-class CpuBackend:
-    device = 'cpu'
-    used = []
-
-    def __init__(self, local_rank):
-        self.index = local_rank
-        self.log = []
-
-    def empty(self, nbytes):
-        return torch.empty(nbytes, dtype=torch.uint8)
-
-    def zeros_i64(self, n):
-        return torch.zeros(max(n, 1), dtype=torch.int64)
-
-    def stream(self):
-        return 0
-
-    def synchronize(self):
-        pass
-
-    def chunker(self, min_len, max_len, key):
-        return OracleChunker(min_len, max_len, key, self.log)
-
-    def fill_streams(self, ptr, n, size, slot, seed, first_id, id_step):
-        from oracle import oracle as o
-        for k in range(n):
-            b = o.fill_splitmix(size, seed, first_id + k * id_step)
-            ctypes.memmove(ptr + k * slot, b.ctypes.data, size)
-
-    def fill_at(self, ptr, nbytes, seed, stream_id, word0):
-        from replicat_amd import synth
-        w = synth.splitmix_words(synth.stream_base(seed, stream_id), word0, (nbytes + 7) // 8)
-        ctypes.memmove(ptr, w.view(np.uint8).ctypes.data, nbytes)
 
 
 def _free_port():
@@ -134,7 +54,7 @@ def _run(argv, world=2):
 
 def test_config2_two_ranks():
     n, mib, steps = 3, 1, 2
-    out = _run(['--config', '2', '--streams', str(n), '--stream-mib', str(mib), '--steps',
+    out = _run(['--gpus', '2', '--config', '2', '--streams', str(n), '--stream-mib', str(mib), '--steps',
                 str(steps), '--warmup', '1', '--cpu-streams', '0', '--min-length', '2000',
                 '--max-length', '80000'])
     from oracle import oracle as o
@@ -163,7 +83,7 @@ def test_config3ii_split_over_two_ranks():
     """One stream split in two windows, chunked per rank, gathered and spliced: every rank ends
     with the whole true cut list of the stream."""
     mib = 4
-    out = _run(['--config', '3ii', '--stream-mib', str(mib), '--steps', '1', '--warmup', '0',
+    out = _run(['--gpus', '2', '--config', '3ii', '--stream-mib', str(mib), '--steps', '1', '--warmup', '0',
                 '--cpu-streams', '0', '--min-length', '2000', '--max-length', '80000'])
     from oracle import oracle as o
     from replicat_amd import synth
@@ -178,10 +98,74 @@ def test_config3ii_split_over_two_ranks():
 def test_parity_flags_gathered_for_config4():
     """Config 4's parity is the AND of every rank's own-shard check; a workload the fixtures do
     not cover (here 2 x 1 MiB per rank) carries no flag on any rank and none in the line."""
-    out = _run(['--config', '4', '--streams', '2', '--stream-mib', '1', '--steps', '1',
+    out = _run(['--gpus', '2', '--config', '4', '--streams', '2', '--stream-mib', '1', '--steps', '1',
                 '--warmup', '0', '--cpu-streams', '0'])
     (_, res0, _, ends0, p0), (_, _, _, ends1, p1) = out
     assert p0 is None and p1 is None  # not the config-4 sizes: no fixture, no flag
     assert res0['parity_sha256'] is None
     # round-robin shards: rank r holds streams r, r + 8
     assert bench.shard_ids('4', 1, 2) == [1, 9]
+
+
+# ------------------------------------------------ bench.py --gpus N as its own launcher
+
+STANDIN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'bench_standin.py')
+SMALL = ['--config', '2', '--streams', '2', '--stream-mib', '1', '--steps', '1', '--warmup', '0',
+         '--cpu-streams', '0', '--min-length', '2000', '--max-length', '80000']
+
+
+def _cli(args, **env_over):
+    """bench.py's command line (bench.cli) over the CPU stand-in, in a fresh process, with no
+    launcher around it: the JSON line (or None) and the exit status."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items()
+           if k not in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_ADDR', 'MASTER_PORT')}
+    env.update(env_over)
+    p = subprocess.run([sys.executable, STANDIN] + args, capture_output=True, text=True,
+                       env=env, timeout=300)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith('{')]
+    return (json.loads(lines[-1]) if lines else None), p.returncode, p.stderr
+
+
+def test_gpus_n_starts_n_ranks():
+    """`bench.py --gpus 2` with no launcher runs two ranks on two distinct devices."""
+    line, rc, err = _cli(['--gpus', '2'] + SMALL)
+    assert rc == 0, err[-2000:]
+    assert line['n_gpus'] == 2 and line['ranks_seen'] == 2
+    assert line['distinct_devices'] == 2 and len(set(line['devices'])) == 2
+    assert line['shared_devices'] is False
+    assert [r['rank'] for r in line['per_rank']] == [0, 1]
+    assert [r['device'] for r in line['per_rank']] == [0, 1]
+    assert all(r['tile_kernel_ms'] == pytest.approx(1.0) for r in line['per_rank'])
+    assert line['roofline']['frac'] is not None
+
+
+def test_gpus_one_runs_in_process():
+    line, rc, err = _cli(['--gpus', '1'] + SMALL)
+    assert rc == 0, err[-2000:]
+    assert line['n_gpus'] == 1 and line['distinct_devices'] == 1 and len(line['per_rank']) == 1
+
+
+def test_shared_devices_refused():
+    """Two ranks, one device: exits non-zero and prints no metric line."""
+    line, rc, _ = _cli(['--gpus', '2'] + SMALL, RC_STANDIN_DEVICES='1')
+    assert rc != 0 and line is None
+
+
+def test_shared_devices_rehearsal_has_no_roofline():
+    line, rc, err = _cli(['--gpus', '2', '--share-gpus'] + SMALL, RC_STANDIN_DEVICES='1')
+    assert rc == 0, err[-2000:]
+    assert line['n_gpus'] == 2 and line['shared_devices'] is True
+    assert line['distinct_devices'] == 1
+    r = line['roofline']
+    assert r['frac'] is None and r['frac_read'] is None and r['achieved'] is None
+    assert 'share a device' in r['note']
+
+
+def test_world_size_must_match_gpus():
+    """A launcher's world size that is not --gpus: exit status 3, no line."""
+    line, rc, err = _cli(['--gpus', '2'] + SMALL, WORLD_SIZE='1', RANK='0', LOCAL_RANK='0')
+    assert rc == 3 and line is None
+    assert '--gpus 2' in err

@@ -28,6 +28,12 @@ def test_exports_every_declared_symbol():
         assert s in _lib.SIGNATURES, f'{s} has no ctypes signature'
 
 
+def test_abi_version_matches_package():
+    import replicat_amd
+    v = _lib.lib().rc_version()
+    assert '%d.%d.%d' % (v // 10000, v // 100 % 100, v % 100) == replicat_amd.__version__
+
+
 def test_tables_match_oracle_clmul(oracle):
     rnd = random.Random(11)
     for _ in range(8):

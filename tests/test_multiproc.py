@@ -5,7 +5,6 @@ import os
 import socket
 
 import pytest
-import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import bench
@@ -20,14 +19,15 @@ def _free_port():
 
 
 def _worker(rank, world, port, q):
-    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
-    dist.init_process_group('gloo', rank=rank, world_size=world)
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), WORLD_SIZE=str(world),
+                      RANK=str(rank), LOCAL_RANK=str(rank))
+    ranks = bench.Ranks()  # bench.py's gloo group
     ids = bench.shard_ids('2', rank, 4)
     ids4 = bench.shard_ids('4', rank, 16)
-    mx = bench.reduce_max([1.0 + rank, 10.0 - rank], dist, 'cpu')
-    dist.barrier()
+    mx = ranks.max([1.0 + rank, 10.0 - rank])
+    ranks.barrier()
     q.put((rank, ids, ids4, mx))
-    dist.destroy_process_group()
+    ranks.close()
 
 
 def test_two_ranks_gloo():
