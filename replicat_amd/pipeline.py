@@ -13,14 +13,22 @@ What it replaces, in /root/reference/replicat/repository.py:
 The stream is gathered into host batches (``batch_bytes``, pinned) exactly as the batching shim
 does (replicat_amd/adapters.py): every batch but the last is chunked as an OPEN prefix (the
 reference's non-final ``next_cut`` calls), the last with its real framing, and the uncut tail
-is carried into the next batch.  Two batches are in flight: the files are read straight into
-one pinned batch (``readinto``) while the device works on the other, each batch on its own HIP
-stream.  Each batch is uploaded ONCE and everything runs on the bytes in HBM: the cut chain (rc_chunk_device), the chunk digests (rc_blake2b_chunks), the per-file
+is carried into the next batch.  ``slots`` batches (default 3) are in flight, each on its own
+HIP stream with its own digest / cipher handles: the files are read straight into one pinned
+batch (``readinto``) while the device works on the others, so the BLAKE2b floor of one batch
+(its longest chunk's chain, ~55 ms for a 5.12 MB chunk) overlaps the next
+batches' uploads, cuts and digests instead of serialising the pipeline.  Each batch is uploaded ONCE and everything runs on the bytes in HBM: the cut chain (rc_chunk_device), the chunk digests (rc_blake2b_chunks), the per-file
 incremental digests of small files (rc_blake2b_update_device: each file's bytes are fed once, in
 the batch that first holds them; a file's state lives in HBM across batches) and, with ``encryption``, every
 chunk's subkey (rc_blake2b_derive_chunks) and its AES-GCM encryption (rc_gcm_encrypt_chunks).
 Only cut offsets, digests and -- what replicat uploads -- the chunk contents come back: sliced
 from the host batch, or the device's nonce || C || T when encrypted.
+
+Memory held per producer: ``slots`` x (one pinned host batch + its HBM copy) of ``capacity`` =
+batch_bytes + max_length + 16 MiB + 128 bytes each (~1.02 GiB at the default 1 GiB batch, so ~3.1
+GiB pinned and ~3.1 GiB HBM with 3 slots); with ``encryption`` each slot also holds a pinned and
+an HBM ciphertext buffer of the same size plus 28 bytes per chunk (~6.1 GiB pinned in all).
+Smaller ``batch_bytes`` or ``slots`` shrink it linearly.
 
 The dedup table and the chunk -> file range map are host bookkeeping on a few integers per
 chunk, as in the reference.  Per-file digests of files of 1 MiB and more are hashed on host
@@ -208,6 +216,10 @@ class _Slot:
 
     def __init__(self, prod, torch):
         dev = prod.dev
+        # per-slot native handles: a handle's staging workspaces are reused every other call, so
+        # a shared one would make the host wait for batch k's digests before queuing batch k + 2's
+        self.hasher = GpuBlake2b(length=prod.digest_size, device=prod.device)
+        self.file_hasher = GpuBlake2b(length=prod.digest_size, device=prod.device)
         self.host = torch.empty(prod.capacity, dtype=torch.uint8, pin_memory=True)
         self.hnp = self.host.numpy()
         self.dbuf = torch.empty(prod.capacity, dtype=torch.uint8, device=dev)
@@ -224,7 +236,17 @@ class _Slot:
             self.d_nonces = torch.empty(total * nb, dtype=torch.uint8, device=dev)
             self.d_enc = torch.empty(max(prod.enc_cap, 1), dtype=torch.uint8, device=dev)
             self.h_enc = torch.empty(max(prod.enc_cap, 1), dtype=torch.uint8, pin_memory=True)
+            from .cipher import GpuAesGcm
+            self.kdf_hasher = GpuBlake2b(length=prod.digest_size, device=prod.device)
+            self.cipher = GpuAesGcm(key_bits=prod.encryption.key_bits,
+                                    nonce_bits=prod.encryption.nonce_bits, device=prod.device)
         self.reset(prod.head)
+
+    def close(self):
+        for h in ('hasher', 'file_hasher', 'kdf_hasher', 'cipher'):
+            obj = getattr(self, h, None)
+            if obj is not None and hasattr(obj, 'close'):
+                obj.close()
 
     def reset(self, head):
         self.off = head          # host offset of the batch's first byte
@@ -244,7 +266,8 @@ class DeviceSnapshotProducer:
     def __init__(self, *, min_length: int = MIN_LENGTH, max_length: int = MAX_LENGTH,
                  params: Optional[bytes] = None, digest_size: int = 64,
                  batch_bytes: int = DEFAULT_BATCH, device=None, keep_contents: bool = True,
-                 encryption: Optional[ChunkEncryption] = None, file_digests: str = 'auto'):
+                 encryption: Optional[ChunkEncryption] = None, file_digests: str = 'auto',
+                 slots: int = 3):
         import torch
         if device is None:
             device = _current_device()
@@ -254,10 +277,8 @@ class DeviceSnapshotProducer:
         self.device = int(device)
         self.dev = torch.device('cuda', self.device)
         self.chunker = GpuChunker(min_length, max_length, normalize_params(params), device=self.device)
-        # one hasher per kind of call: each makes one call per batch, so the two workspaces
-        # a handle alternates between (capi_digest.cpp) are never those of a batch in flight
-        self.hasher = GpuBlake2b(length=digest_size, device=self.device)
-        self.file_hasher = GpuBlake2b(length=digest_size, device=self.device)
+        if int(slots) < 2:
+            raise ValueError('slots must be at least 2 (one batch filled while one is on the device)')
         self.min_length, self.max_length = min_length, max_length
         self.digest_size = digest_size
         self.batch_bytes = max(int(batch_bytes), 2 * max_length + 16)
@@ -275,15 +296,16 @@ class DeviceSnapshotProducer:
         self.encryption = encryption
         if encryption is not None:
             from .cipher import GpuAesGcm
-            self.kdf_hasher = GpuBlake2b(length=digest_size, device=self.device)
+            # the layout of the ciphertexts (nonce || C || T per chunk); each slot encrypts with
+            # its own handle
             self.cipher = GpuAesGcm(key_bits=encryption.key_bits, nonce_bits=encryption.nonce_bits,
                                     device=self.device)
             kdf = state_init(self.cipher.key_bytes, key=encryption.shared_key,
                              salt=encryption.shared_kdf_params)
             self.d_kdf = torch.from_numpy(np.frombuffer(kdf, dtype=np.uint8).copy()).to(self.dev)
             self.enc_cap, _ = self.cipher.chunks_layout(self.chunker, [self.capacity])
-        # two batches in flight: the host fills one while the device works on the other
-        self._slots = [_Slot(self, torch) for _ in range(2)]
+        # `slots` batches in flight: the host fills one while the device works on the others
+        self._slots = [_Slot(self, torch) for _ in range(int(slots))]
         self._look = bytearray(PIECE)  # the piece after a full batch (tells whether it is final)
 
     # ------------------------------------------------------------------- file digests
@@ -319,8 +341,10 @@ class DeviceSnapshotProducer:
             if pool is not None:
                 pool.shutdown(wait=True)
         self._pool = self._collect_pool = None
+        for sl in self._slots:
+            sl.close()
         self._slots = []
-        for h in ('chunker', 'hasher', 'file_hasher', 'kdf_hasher', 'cipher'):
+        for h in ('chunker', 'cipher'):
             obj = getattr(self, h, None)
             if obj is not None and hasattr(obj, 'close'):
                 obj.close()
@@ -367,16 +391,17 @@ class DeviceSnapshotProducer:
         prev, look, k = None, None, 0
         # records are built on a collector thread (they copy chunk contents, holding the GIL)
         # while this thread reads the next batch (the reads release it)
-        collected = [None, None]  # per slot: the collection of its last batch
+        ns = len(self._slots)
+        collected = [None] * ns  # per slot: the collection of its last batch
         collector = self._collector()
         try:
             look = reader.read_into(self._look)
             while True:
-                s = self._slots[k & 1]
-                if collected[k & 1] is not None:  # the slot's previous batch is fully consumed
+                s = self._slots[k % ns]
+                if collected[k % ns] is not None:  # the slot's previous batch is fully consumed
                     t = clock()
-                    collected[k & 1].result()
-                    collected[k & 1] = None
+                    collected[k % ns].result()
+                    collected[k % ns] = None
                     prof['collect_join'] += clock() - t
                 s.reset(self.head)
                 # ---- fill: the piece read ahead, then whole pieces up to batch_bytes of new bytes
@@ -409,9 +434,9 @@ class DeviceSnapshotProducer:
                 prof['batches'] += 1
                 prof['enqueue'] += clock() - t2
                 if prev is not None:
-                    collected[(k - 1) & 1] = collector.submit(run.collect, prev)
+                    collected[(k - 1) % ns] = collector.submit(run.collect, prev)
                 if s.final:
-                    collected[k & 1] = collector.submit(run.collect, s)
+                    collected[k % ns] = collector.submit(run.collect, s)
                     for f in collected:
                         if f is not None:
                             f.result()
@@ -456,8 +481,10 @@ class _Run:
         self.hstates[fi].push(memoryview(s.hnp)[at:at + n], s.host_jobs, self.p._host_pool())
 
     def enqueue(self, s, prev, T, last_start, new_lo, new_hi):
-        """Upload batch s and queue its cuts, chunk digests, subkeys + ciphertexts and the
-        device file digests of its new bytes on s.stream."""
+        """Upload batch s and queue, on s.stream: its cuts, the device file digests of its new
+        bytes, its chunk digests, and subkeys + ciphertexts.  The file digests go before the
+        chunk digests: the next batch's file digests wait for them (a file's state advances
+        batch after batch), and must not wait behind this batch's ~55 ms digest floor."""
         torch, p = self.torch, self.p
         hs = s.stream.cuda_stream
         ptr = s.dbuf.data_ptr()
@@ -471,20 +498,6 @@ class _Run:
             last = torch.index_select(s.d_cuts, 0, (s.d_count - 1).clamp_(min=0))
             s.h_meta[1:2].copy_(last, non_blocking=True)
             s.ev_cut.record(s.stream)
-            p.hasher.digest_chunks(p.chunker, [ptr], [s.blen], s.d_cuts.data_ptr(),
-                                   s.d_count.data_ptr(), s.d_digests.data_ptr(), hs)
-            if p.encryption is not None:
-                # derive_shared_subkey(digest) and encrypt, per chunk, still in HBM; one
-                # os.urandom nonce per chunk as the adapter draws them (adapters.py:133)
-                p.kdf_hasher.derive_chunks(p.chunker, [s.blen], s.d_count.data_ptr(),
-                                           p.d_kdf.data_ptr(), s.d_digests.data_ptr(),
-                                           s.d_keys.data_ptr(), hs)
-                s.h_nonces.numpy()[:] = np.frombuffer(os.urandom(s.h_nonces.numel()),
-                                                      dtype=np.uint8)
-                s.d_nonces.copy_(s.h_nonces, non_blocking=True)
-                p.cipher.encrypt_chunks(p.chunker, [ptr], [s.blen], s.d_cuts.data_ptr(),
-                                        s.d_count.data_ptr(), s.d_keys.data_ptr(),
-                                        s.d_nonces.data_ptr(), s.d_enc.data_ptr(), hs)
             # device file digests over the new bytes [T, blen): a file's state in HBM is
             # advanced batch after batch, so this stream first waits for the previous batch's
             # (files below prev.closed were closed by earlier batches, collected or not)
@@ -509,14 +522,30 @@ class _Run:
                     else:
                         self.states[fi].record_stream(s.stream)
                 scratch = torch.zeros((len(items), SLOT), dtype=torch.uint8, device=p.dev)
-                p.file_hasher.update_device([self.states[fi].data_ptr() for fi, _, _, _ in items],
+                s.file_hasher.update_device([self.states[fi].data_ptr() for fi, _, _, _ in items],
                                             [q for _, q, _, _ in items],
                                             [n for _, _, n, _ in items],
                                             [1 if fin else 0 for _, _, _, fin in items],
                                             scratch.data_ptr(), hs)
                 s.file_digests = scratch
                 s.items = [(fi, fin) for fi, _, _, fin in items]
+            elif prev is not None:
+                s.stream.wait_event(prev.ev_upd)  # keep the file-state order transitive
             s.ev_upd.record(s.stream)
+            s.hasher.digest_chunks(p.chunker, [ptr], [s.blen], s.d_cuts.data_ptr(),
+                                   s.d_count.data_ptr(), s.d_digests.data_ptr(), hs)
+            if p.encryption is not None:
+                # derive_shared_subkey(digest) and encrypt, per chunk, still in HBM; one
+                # os.urandom nonce per chunk as the adapter draws them (adapters.py:133)
+                s.kdf_hasher.derive_chunks(p.chunker, [s.blen], s.d_count.data_ptr(),
+                                           p.d_kdf.data_ptr(), s.d_digests.data_ptr(),
+                                           s.d_keys.data_ptr(), hs)
+                s.h_nonces.numpy()[:] = np.frombuffer(os.urandom(s.h_nonces.numel()),
+                                                      dtype=np.uint8)
+                s.d_nonces.copy_(s.h_nonces, non_blocking=True)
+                s.cipher.encrypt_chunks(p.chunker, [ptr], [s.blen], s.d_cuts.data_ptr(),
+                                        s.d_count.data_ptr(), s.d_keys.data_ptr(),
+                                        s.d_nonces.data_ptr(), s.d_enc.data_ptr(), hs)
             s.ev_done.record(s.stream)
 
     def collect(self, s):
