@@ -1,24 +1,29 @@
 // kernels.hip -- gfx950 kernels of the content-defined chunker.
 //
 // Replaces the scan of /root/reference/src/adapters.cpp:42-77 (next_cut's argmax over key())
-// with two launches per batch of streams:
+// with, per batch of streams:
 //
-//   phase A  tile kernel   (HBM-bound, one pass over every input byte)
-//            Every wave owns 2048-key tiles (8 KiB of stream) and reduces each to one
+//   tile kernel  (HBM-bound, one pass over every needed input byte)  rc_tile_kernel<G>
+//            Persistent: one 1024-thread workgroup per CU, each wave a contiguous range of
+//            4096-key tiles (16 KiB of stream, kTileKeys in gclmul.h), reduced to one
 //            TileRecord = (first maximal 64-bit key, its index).  Bytes stream straight from
-//            HBM into registers with coalesced 16-byte loads (1 KiB per wave instruction).
-//            Per key it evaluates only the top 16 bits of the hash: 4 conflict-free LDS
-//            lookups per 32-bit word (replicated prefilter tables, see gclmul.h) + DPP for the
-//            neighbour word.  Each lane keeps the first and the last index of its largest
-//            top-16 value; the exact 64-bit key is computed once per lane, the wave reduces
-//            (key desc, index asc).  A lane whose top-16 maximum occurs twice and could be the
-//            tile maximum sends the tile down the exact path (rare on random data).
+//            HBM into a register ring (16 x 16-byte buffer loads per lane in flight).  Per key
+//            only the top 16 bits of the hash are evaluated: 4 conflict-free LDS lookups per
+//            32-bit word (32x replicated prefilter tables, see gclmul.h), one v_bitop3 fold, DPP
+//            for the neighbour word.  The wave's candidate lanes (their top-16 maximum is the
+//            tile's) get the exact 64-bit key one tile later.  A candidate lane whose maximum
+//            occurs twice makes the tile a marker record, resolved by rc_edge_kernel from the
+//            candidate lanes.  G = 4 also stores per-quarter group bounds (small windows).
 //
-//   phase B  chain kernel  (latency-bound, tiny)
-//            One wave per stream walks the cut chain exactly as replicat's adapter loop does
+//   edge kernel  rc_edge_kernel: marker tiles and the tiles that run past a stream's end.
+//
+//   chain        (latency-bound)  the cut chain exactly as replicat's adapter loop cuts
 //            (tail rules of adapters.cpp:48-57 under the piece framing of adapters.py:290-305):
-//            the argmax window [s+4, s+max) is the maximum over the tile records fully inside
-//            it plus the exact keys of the two partial edge tiles.
+//            each argmax window [s+4, s+max) is the maximum over the records of the tiles fully
+//            inside it plus its two partial edge ranges.  Default for batches of >= 256 small-
+//            window streams: a QUAD of lanes per stream (rc_quad_chain_kernel); otherwise one
+//            wave per segment (rc_spec_kernel: speculative chains over segments of long
+//            streams, spliced by rc_join_kernel / rc_merge / rc_scan / rc_copy).
 //
 // No MFMA anywhere: this is integer byte work.
 #include <hip/hip_runtime.h>
@@ -506,6 +511,12 @@ __device__ __forceinline__ GroupRecord tile_groups(const uint32_t (&gpk)[(G + 1)
     return r;
 }
 
+#ifdef RC_DIAG_TILE_STAMPS
+// diagnostic build only: per wave of the tile kernel, s_memrealtime (100 MHz) when its first tile
+// starts and when its last record is stored, and its tile count (scripts/tile_stamps.py)
+__device__ uint64_t g_tile_stamp[3 * 8192];
+#endif
+
 // Persistent: one 1024-thread workgroup per CU, each wave a contiguous range of tiles.
 // G > 1: also grp[t] = the tile's group bounds (GroupRecord: the top-16 maximum of each of its
 // G key groups, keys that do not exist counting as 0, and the maximum outside the lane holding
@@ -542,6 +553,9 @@ __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restri
         return;
     }
 
+#ifdef RC_DIAG_TILE_STAMPS
+    const uint64_t stamp0 = __builtin_amdgcn_s_memrealtime();
+#endif
     TileCursor<G == 1> cursor;
     cursor.init(d, n_streams, t);
     TileRef cur = cursor.at(t);
@@ -656,6 +670,13 @@ __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restri
             rec[pend_t].key = bk;
             rec[pend_t].j = bj;
             xcount[gw] = n_ties;
+#ifdef RC_DIAG_TILE_STAMPS
+            if (gw < 8192) {
+                g_tile_stamp[3 * gw] = stamp0;
+                g_tile_stamp[3 * gw + 1] = __builtin_amdgcn_s_memrealtime();
+                g_tile_stamp[3 * gw + 2] = t_end - t_begin;
+            }
+#endif
         }
     }
 }
@@ -2567,6 +2588,15 @@ int cu_count() {
 extern "C" {
 
 const char *rc_launch_error(void) { return g_launch_err; }
+
+#ifdef RC_DIAG_TILE_STAMPS
+int rc_diag_tile_read(uint64_t *out, uint32_t waves) {
+    if (waves > 8192) waves = 8192;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tile_stamp), 3 * 8 * (size_t)waves) != hipSuccess) return 1;
+    static uint64_t zero[3 * 8192];
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_tile_stamp), zero, sizeof zero) != hipSuccess;
+}
+#endif
 
 #ifdef RC_DIAG_STAMPS
 int rc_diag_read(uint64_t *out, uint32_t cap, uint32_t *n) {

@@ -2,6 +2,7 @@
 #   1. scripts/placement_probe2.py 6: one launch vs k launches, tile orders, per allocation
 #   2. digest_overlap_probe.py with GPU_MAX_HW_QUEUES=8 (is 4 queues what caps 3-4 slots?)
 #   3. one --pmc pass asking for TCC_EA0_RDREQ without _sum (per-channel rows or not?)
+#   4. scripts/tile_stamps.py (diag/lib_TSTAMPS.so): when each tile-kernel wave ends
 set -u
 cd "$GRAFT_REPO_ROOT"
 out=gpurun_out/probe_c
@@ -16,4 +17,7 @@ rc=$?; echo "overlap q8 rc=$rc"; grep '^{' $out/digest_overlap_q8.log
 timeout -k 10 120 rocprofv3 --pmc TCC_EA0_RDREQ -d $out/pmc_tcc -o run --output-format csv \
     -- python3 -u scripts/placement_probe2.py 1 > $out/pmc_tcc.log 2>&1
 rc=$?; echo "pmc tcc rc=$rc"
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 200 python -u scripts/tile_stamps.py > $out/tile_stamps.log 2>&1
+rc=$?; echo "stamps rc=$rc"; grep '^{' $out/tile_stamps.log | cut -c1-700
 exit $rc

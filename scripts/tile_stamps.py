@@ -1,0 +1,64 @@
+"""Diagnostic: when each wave of the tile kernel starts and ends (diag/lib_TSTAMPS.so, built with
+-DRC_DIAG_TILE_STAMPS).  The kernel gives every wave the same number of tiles; how far apart the
+waves finish is the time a dynamic tile hand-out could recover at the end of the launch.
+
+    python -m replicat_amd.build --variant TSTAMPS -DRC_DIAG_TILE_STAMPS
+    python scripts/tile_stamps.py [n_streams] [stream_mib] [min] [max]     (default: config 2)
+"""
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ['RC_LIB_PATH'] = os.path.join(ROOT, 'diag', 'lib_TSTAMPS.so')
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from replicat_amd import _lib, synth  # noqa: E402
+from replicat_amd.chunker import GpuChunker, fill_splitmix_streams  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+size = (int(sys.argv[2]) if len(sys.argv) > 2 else 64) << 20
+mn = int(sys.argv[3]) if len(sys.argv) > 3 else 128_000
+mx = int(sys.argv[4]) if len(sys.argv) > 4 else 5_120_000
+ch = GpuChunker(mn, mx, b'\xff' * 16)
+pool = torch.empty(n * size + 64, dtype=torch.uint8, device='cuda')
+ptrs = [pool.data_ptr() + i * size for i in range(n)]
+hs = torch.cuda.current_stream().cuda_stream
+fill_splitmix_streams(pool.data_ptr(), n, size, size, synth.DEFAULT_SEED, 0, 1, hs)
+total, caps = ch.capacity([size] * n)
+cuts = torch.zeros(total, dtype=torch.int64, device='cuda')
+counts = torch.zeros(n, dtype=torch.int64, device='cuda')
+L = _lib.lib()
+L.rc_diag_tile_read.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+waves = torch.cuda.get_device_properties(0).multi_processor_count * 16
+for rep in range(4):
+    ch.timing(True)
+    ch.chunk_device(ptrs, [size] * n, None, cuts.data_ptr(), counts.data_ptr(), hs)
+    torch.cuda.synchronize()
+    ch.timing(False)
+    tile_ms = ch.read_kernel_timing()[0]
+    buf = np.zeros(3 * waves, np.uint64)
+    assert L.rc_diag_tile_read(buf.ctypes.data, waves) == 0
+    s, e, k = buf[0::3].astype(np.int64), buf[1::3].astype(np.int64), buf[2::3]
+    ok = e > 0
+    s, e, k = s[ok], e[ok], k[ok]
+    t0 = s.min()
+    ends = (e - t0) / 100.0  # us (100 MHz)
+    starts = (s - t0) / 100.0
+    dur = ends - starts
+    wg = np.nonzero(ok)[0] // 16
+    xcd = wg % 8
+    per_xcd = {int(x): round(float(np.median(ends[xcd == x])), 1) for x in range(8)}
+    q = np.percentile(ends, [0, 1, 10, 50, 90, 99, 100])
+    print(json.dumps({'rep': rep, 'tile_kernel_ms': round(tile_ms, 3), 'waves': int(ok.sum()),
+                      'tiles_per_wave': [int(k.min()), int(k.max())],
+                      'start_us_max': round(float(starts.max()), 1),
+                      'end_us_percentiles_0_1_10_50_90_99_100': [round(float(x), 1) for x in q],
+                      'tail_us_after_median_end': round(float(q[-1] - q[3]), 1),
+                      'tail_frac_of_last_end': round(float((q[-1] - q[3]) / q[-1]), 4),
+                      'duration_us_min_med_max': [round(float(x), 1) for x in
+                                                  (dur.min(), np.median(dur), dur.max())],
+                      'median_end_by_xcd_us': per_xcd}), flush=True)
