@@ -25,7 +25,12 @@ SOURCES = [os.path.join(CSRC, n) for n in ('kernels.hip', 'capi.cpp', 'blake2b.h
 HEADERS = [os.path.join(CSRC, n) for n in ('gclmul.h', 'digest_kernels.h', 'capi_internal.h', 'cipher_kernels.h')] + [
     os.path.join(ROOT, 'include', n) for n in ('replicat_chunker.h', 'replicat_digest.h', 'replicat_cipher.h')]
 ARCH = 'gfx950'
-FLAGS = [f'--offload-arch={ARCH}', '-O3', '-std=c++17', '-fPIC', '-shared', '-Wall']
+# -amdgpu-atomic-optimizer-strategy=None: the tile kernel's one-lane grab of its next work unit
+# must stay a plain global_atomic_add whose result is read a unit later; the optimizer rewrites a
+# uniform-address atomic into a wave reduction + readfirstlane, i.e. an immediate vmcnt(0) that
+# drains the wave's whole HBM ring (kernels.hip TileUnits)
+FLAGS = [f'--offload-arch={ARCH}', '-O3', '-std=c++17', '-fPIC', '-shared', '-Wall',
+         '-mllvm', '-amdgpu-atomic-optimizer-strategy=None']
 _ID_RE = re.compile(rb'RC_BUILD_ID:([0-9a-f]{16})')
 
 

@@ -361,6 +361,10 @@ int stage_descriptors(rc_chunker *ch, Workspace &ws, uint64_t n, const uint8_t *
     }
     u[5 * n] = tiles;
     u[8 * n + 1] = segs;
+    // tile indices are 32-bit in the tile kernel's units and tie lists (kernels.hip TileUnits):
+    // 2^32 tiles = 64 TiB of stream per call
+    if (tiles >= (1ull << 32) - (1ull << 20))
+        return fail(RC_ERR_ARGUMENT, "too many bytes in one call: %llu tiles", (unsigned long long)tiles);
     plan.n_tiles = tiles;
     plan.total_cap = cuts;
     plan.n_segs = segs;
@@ -373,14 +377,14 @@ GroupRecord *group_records(Workspace &ws, const Plan &plan) {
                                            (plan.n_tiles + 1) * sizeof(TileRecord));
 }
 
-// the tile kernel's per-wave tie lists: n_tiles slots + one count per wave (<= n_tiles + 16)
+// the tile kernel's tie lists: n_tiles slots, one count per work unit, the grab counter
 uint32_t *tie_lists(Workspace &ws, const Plan &plan) {
     return reinterpret_cast<uint32_t *>(group_records(ws, plan) + plan.n_tiles + 1);
 }
 
 size_t records_bytes(const Plan &plan) {
     return (plan.n_tiles + 1) * (sizeof(TileRecord) + sizeof(GroupRecord)) +
-           (2 * plan.n_tiles + 32) * 4;
+           rc_tie_list_words(plan.n_tiles) * 4;
 }
 
 // batches of at least this many streams walk their chains one lane per stream (when the
@@ -539,6 +543,9 @@ int rc_chunker_create(uint64_t min_length, uint64_t max_length, const uint8_t *k
     ch->small = ch->window / kTileKeys + 3 <= 64;
     ch->groups = ch->small;
     if (const char *e = getenv("RC_TILE_GROUPS_OFF")) ch->groups = ch->groups && e[0] != '1';
+    // RC_TILE_GROUPS_ON=1: group records for large windows too (the chains trim their edge
+    // ranges with them, chain_step); measured before it becomes a default
+    if (const char *e = getenv("RC_TILE_GROUPS_ON")) ch->groups = ch->groups || e[0] == '1';
     if (const char *e = getenv("RC_CHAIN_LEAN_OFF")) ch->small = ch->small && e[0] != '1';
     ch->k0 = k0;
     ch->k1 = k1;

@@ -126,11 +126,12 @@ extern "C" {
 // d_grp (may be NULL): n_tiles + 1 group records (per-group top-16 bounds, GroupRecord) --
 // the chain's bounds for small windows.  mid_event (a hipEvent_t, may be NULL):
 // recorded between the tile and the edge kernel.
-// d_xlist: n_tiles + (one count per tile-kernel wave: at most n_tiles) u32 of scratch for the
-// tile kernel's per-wave tie lists.
+// d_xlist: rc_tie_list_words(n_tiles) u32 of scratch: the tile kernel's tie lists (n_tiles
+// slots), one count per work unit and the dynamic units' grab counter (zeroed per launch).
 int rc_launch_tiles(const rc::KeyTables *d_tables, rc::StreamDesc desc, uint64_t n_streams,
                     uint64_t n_tiles, rc::TileRecord *d_records, rc::GroupRecord *d_grp,
                     uint32_t hot, uint32_t *d_xlist, void *stream, void *mid_event);
+uint64_t rc_tie_list_words(uint64_t n_tiles);
 int rc_launch_chain(const rc::KeyTables *d_tables, rc::StreamDesc desc, uint64_t n_streams,
                     rc::ChainParams prm, uint64_t n_segs, const rc::TileRecord *d_records,
                     uint64_t *d_cuts, int64_t *d_counts, uint64_t *d_scratch,

@@ -517,52 +517,127 @@ __device__ __forceinline__ GroupRecord tile_groups(const uint32_t (&gpk)[(G + 1)
 __device__ uint64_t g_tile_stamp[3 * 8192];
 #endif
 
-// Persistent: one 1024-thread workgroup per CU, each wave a contiguous range of tiles.
+// The tile kernel's work units (round 3): wave w first takes the static unit w, tiles
+// [w s0, (w + 1) s0); the rest of the tiles, from dyn0 = nw s0 on, are dynamic units of `chunk`
+// tiles that waves grab from a counter (one atomic per unit) when they run out of work.  Round 2
+// gave every wave the same static share and measured (RC_DIAG_TILE_STAMPS) the waves of one
+// launch ending between 52 % and 100 % of its time: the slowest waves' tail was ~23 % of the
+// kernel.  Small launches (fewer than kDynMinPerWave tiles per wave) stay fully static.
+// Static share 25 %, units of 32 tiles (tile_units): the tile kernel 10-11 % faster on configs 2,
+// 3 (iii) and 4 than fully static on the same allocation.
+struct TileUnits {  // tile indices fit 32 bits (the tie lists store them as u32)
+    uint32_t n_tiles, nw, s0, chunk, dyn0, n_units;
+    __device__ __host__ void range(uint32_t u, uint32_t &b, uint32_t &e) const {
+        if (u < nw) {
+            b = u * s0;
+            e = b + s0;
+        } else {
+            b = dyn0 + (u - nw) * chunk;
+            e = b + chunk;
+        }
+        if (b > n_tiles) b = n_tiles;
+        if (e > n_tiles) e = n_tiles;
+    }
+};
+
+// Units of a launch over n_tiles tiles by nw waves.  RC_TILE_STATIC (per mille, default 250): the
+// share of the tiles handed out statically; RC_TILE_CHUNK (default 32): dynamic unit size.  Both
+// measured on one allocation per config (scripts/tile_sched_ab.py, profiles/r03/sched): tile
+// kernel vs the round-2 fully static schedule, config 2 11.06 -> 9.88 ms, 3 (iii) 11.46 -> 10.32,
+// config 4 23.87 -> 21.23; the harness (76 tiles per wave) is fastest fully static.
+constexpr uint64_t kDynMinPerWave = 128;  // fewer tiles per wave: one static unit each
+constexpr uint64_t kDynChunkMin = 2;    // units of at least 2 tiles
+__host__ inline TileUnits tile_units(uint64_t n_tiles, uint64_t nw) {
+    TileUnits U;
+    U.n_tiles = (uint32_t)n_tiles;
+    U.nw = (uint32_t)nw;
+    uint64_t permille = 250, chunk = 32;
+    if (const char *e = getenv("RC_TILE_STATIC")) permille = strtoull(e, nullptr, 0);
+    if (const char *e = getenv("RC_TILE_CHUNK")) chunk = strtoull(e, nullptr, 0);
+    if (permille > 1000) permille = 1000;
+    if (chunk < kDynChunkMin) chunk = kDynChunkMin;
+    if (n_tiles < kDynMinPerWave * nw || permille == 1000) {  // fully static
+        U.s0 = (uint32_t)((n_tiles + nw - 1) / nw);
+        U.chunk = 1;
+        U.dyn0 = (uint32_t)n_tiles;
+        U.n_units = (uint32_t)nw;
+        return U;
+    }
+    U.s0 = (uint32_t)(n_tiles * permille / 1000 / nw);
+    // at least ~4 dynamic units per wave: a unit is the granularity of the launch's tail
+    const uint64_t dyn = n_tiles - nw * U.s0, fit = dyn / (4 * nw);
+    if (chunk > fit) chunk = fit > kDynChunkMin ? fit : kDynChunkMin;
+    U.chunk = (uint32_t)chunk;
+    U.dyn0 = (uint32_t)(nw * U.s0);
+    U.n_units = (uint32_t)(nw + (n_tiles - U.dyn0 + chunk - 1) / chunk);
+    return U;
+}
+
+// Persistent: one 1024-thread workgroup per CU, each wave its static unit, then dynamic units.
 // G > 1: also grp[t] = the tile's group bounds (GroupRecord: the top-16 maximum of each of its
 // G key groups, keys that do not exist counting as 0, and the maximum outside the lane holding
 // it), upper bounds the chains use to leave most of an edge range unscanned (chain_step,
 // rc_lane_chain_kernel).
 //
 // Tiles the fast path cannot settle -- a candidate lane holding its top-16 maximum twice --
-// are listed per wave for the edge kernel: xlist[t_begin + i] (i < xcount[wave]).  Every tile
-// stores its index at the list's next slot and only a tie advances the count, so the store is
-// unconditional and every tile keeps the same vector-memory sequence.
+// are listed per unit for the edge kernel: xlist[b + i] (i < xcount[u], b the unit's first
+// tile).  Every tile stores its index at its unit's next slot and only a tie advances the count,
+// so the store is unconditional and every tile keeps the same vector-memory sequence.
+//
+// The grab for a wave's next unit is issued when it enters a unit and read when it leaves it,
+// so the atomic's latency hides behind the unit's tiles.  ctr must be 0 at launch.
 template <int G>
 __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restrict__ tab,
                                                        StreamDesc d, uint64_t n_streams,
-                                                       uint64_t n_tiles,
+                                                       TileUnits U,
                                                        TileRecord *__restrict__ rec,
                                                        GroupRecord *__restrict__ grp,
                                                        uint32_t hot,
                                                        uint32_t *__restrict__ xlist,
-                                                       uint32_t *__restrict__ xcount) {
+                                                       uint32_t *__restrict__ xcount,
+                                                       uint32_t *__restrict__ ctr) {
     stage_tile_tables(tab);
     const uint64_t *full = reinterpret_cast<const uint64_t *>(s_tile_lds + kFullOff / 4);
     const uint64_t *tl = full, *th = full + 1024;
+    const uint64_t n_tiles = U.n_tiles;
 
     const uint32_t lane = lane_id();
     const uint32_t lb_a = (lane & 31) * 4, lb_b = lb_a | 0x10000u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t gw = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
-    const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    uint64_t t = n_tiles * gw / nw;
-    const uint64_t t_begin = t, t_end = n_tiles * (gw + 1) / nw;
+    const bool dynamic = U.n_units > U.nw;
+    // the grab of the next unit: lane 0's atomic, read (readfirstlane) only when it is needed
+    uint32_t grab_v = 0;
+    if (dynamic && lane == 0) grab_v = atomicAdd(ctr, 1u);
+    uint32_t u = (uint32_t)gw, ub, ue;
+    U.range(u, ub, ue);
     uint32_t n_ties = 0;
-    if (t >= t_end) {
-        if (lane == 0) xcount[gw] = 0;
-        return;
-    }
-
 #ifdef RC_DIAG_TILE_STAMPS
     const uint64_t stamp0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t n_done = 0;
 #endif
+
+    // the first fast tile, possibly in a later unit (units without one list no ties)
     TileCursor<G == 1> cursor;
-    cursor.init(d, n_streams, t);
-    TileRef cur = cursor.at(t);
-    while (!cur.fast && ++t < t_end) cur = cursor.at(t);
-    if (!cur.fast) {  // no fast tile at all (the host lists the tiles that are not fast)
-        if (lane == 0) xcount[gw] = 0;
-        return;
+    TileRef cur;
+    uint64_t t = ub;
+    bool seek = true;
+    for (;;) {
+        if (t < ue) {
+            if (seek) cursor.init(d, n_streams, t);
+            seek = false;
+            cur = cursor.at(t);
+            if (cur.fast) break;
+            ++t;
+            continue;
+        }
+        if (lane == 0) xcount[u] = 0;
+        u = dynamic ? U.nw + (uint32_t)__builtin_amdgcn_readfirstlane(grab_v) : U.n_units;
+        if (u >= U.n_units) return;
+        U.range(u, ub, ue);
+        if (lane == 0) grab_v = atomicAdd(ctr, 1u);
+        t = ub;
+        seek = true;
     }
     u32x4 x[kTileIters];
     // the word before the first tile (tile 0 of a stream has none: key 0 is masked)
@@ -586,12 +661,28 @@ __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restri
     uint32_t pend_lo = 0, pend_hi = 0, pend_jl = 0;  // per lane: candidate words and index
 
     for (;;) {
+        // the next fast tile: in this unit, else in the next units (grabbed ones)
         TileRef nx = cur;
         nx.fast = false;
         uint64_t tn = t + 1;
-        for (; tn < t_end; ++tn) {
-            nx = cursor.at(tn);
-            if (nx.fast) break;
+        uint32_t nu = u, nub = ub, nue = ue;
+        for (;;) {
+            if (tn < nue) {
+                nx = cursor.at(tn);
+                if (nx.fast) break;
+                ++tn;
+                continue;
+            }
+            if (nu != u && lane == 0) xcount[nu] = 0;  // a grabbed unit without a fast tile
+            nu = dynamic ? U.nw + (uint32_t)__builtin_amdgcn_readfirstlane(grab_v) : U.n_units;
+            if (nu >= U.n_units) {
+                nu = u;  // no more work: cur is the wave's last tile
+                break;
+            }
+            U.range(nu, nub, nue);
+            if (lane == 0) grab_v = atomicAdd(ctr, 1u);
+            tn = nub;
+            if (tn < nue) cursor.init(d, n_streams, tn);
         }
         uint32_t top, first, last;
         uint32_t gpk[(G + 1) / 2];
@@ -634,7 +725,7 @@ __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restri
         const uint64_t cmask = __ballot(cand);
         const bool tie = __any(cand && first != last);
         const uint32_t win = 0xffffu - (p & 0xffffu);
-        if (lane == 0) xlist[t_begin + n_ties] = (uint32_t)t;  // kept only if it is a tie
+        if (lane == 0) xlist[ub + n_ties] = (uint32_t)t;  // kept only if it is a tie
         n_ties += tie ? 1u : 0u;
         pend_t = t;
         pend_j0 = cur.j0;
@@ -647,7 +738,16 @@ __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restri
 #else
         if (lane == 0 && (top ^ first ^ last) == 0x5a5au) rec[t].key = first ^ last;  // keep the scan alive
 #endif
-
+#ifdef RC_DIAG_TILE_STAMPS
+        ++n_done;
+#endif
+        if (nu != u) {  // cur was its unit's last fast tile: close the unit's tie list
+            if (lane == 0) xcount[u] = n_ties;
+            n_ties = 0;
+            u = nu;
+            ub = nub;
+            ue = nue;
+        }
         if (!nx.fast) break;
         t = tn;
         cur = nx;
@@ -669,12 +769,12 @@ __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restri
         if (lane == 0) {
             rec[pend_t].key = bk;
             rec[pend_t].j = bj;
-            xcount[gw] = n_ties;
+            xcount[u] = n_ties;
 #ifdef RC_DIAG_TILE_STAMPS
             if (gw < 8192) {
                 g_tile_stamp[3 * gw] = stamp0;
                 g_tile_stamp[3 * gw + 1] = __builtin_amdgcn_s_memrealtime();
-                g_tile_stamp[3 * gw + 2] = t_end - t_begin;
+                g_tile_stamp[3 * gw + 2] = n_done;
             }
 #endif
         }
@@ -750,29 +850,30 @@ __device__ __forceinline__ void exact_lanes(const uint64_t *tl, const uint64_t *
 // over the same key range the fast path would have covered (tile_key_end).
 __global__ __launch_bounds__(256) void rc_edge_kernel(const KeyTables *__restrict__ tab,
                                                       StreamDesc d, uint64_t n_streams,
-                                                      uint64_t n_tiles,
+                                                      TileUnits U,
                                                       TileRecord *__restrict__ rec,
                                                       GroupRecord *__restrict__ grp,
                                                       const uint32_t *__restrict__ xlist,
-                                                      const uint32_t *__restrict__ xcount,
-                                                      uint64_t n_waves) {
+                                                      const uint32_t *__restrict__ xcount) {
     __shared__ __attribute__((aligned(16))) uint64_t s_full[2048];
     const uint64_t gw = (uint64_t)blockIdx.x * (blockDim.x >> 6) +
                         __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
     const uint64_t n_host = sload(d.xtiles);
+    const uint64_t n_units = U.n_units;
     // almost every workgroup has nothing to recompute: it leaves before staging the tables
     bool work = false;
-    for (uint64_t e = gw; e < n_waves + n_host && !work; e += nw)
-        work = e >= n_waves || __builtin_amdgcn_readfirstlane(xcount[e]) != 0;
+    for (uint64_t e = gw; e < n_units + n_host && !work; e += nw)
+        work = e >= n_units || __builtin_amdgcn_readfirstlane(xcount[e]) != 0;
     if (!__syncthreads_or(work)) return;
     const uint64_t *gfull = &tab->tl[0][0];
     for (uint32_t i = threadIdx.x; i < 2048u; i += blockDim.x) s_full[i] = gfull[i];
     __syncthreads();
     const uint64_t *tl = s_full, *th = s_full + 1024;
-    for (uint64_t e = gw; e < n_waves + n_host; e += nw) {
-        if (e < n_waves) {
-            const uint64_t t0 = n_tiles * e / n_waves;
+    for (uint64_t e = gw; e < n_units + n_host; e += nw) {
+        if (e < n_units) {
+            uint32_t t0, t1;
+            U.range((uint32_t)e, t0, t1);
             const uint32_t c = (uint32_t)__builtin_amdgcn_readfirstlane(xcount[e]);
             for (uint32_t i = 0; i < c; ++i) {
                 const uint64_t t = (uint32_t)__builtin_amdgcn_readfirstlane(xlist[t0 + i]);
@@ -784,7 +885,7 @@ __global__ __launch_bounds__(256) void rc_edge_kernel(const KeyTables *__restric
                     exact_tile(tl, th, d, s, t, rec, grp);
             }
         } else {
-            const uint64_t t = sload(d.xtiles + 1 + (e - n_waves));
+            const uint64_t t = sload(d.xtiles + 1 + (e - n_units));
             exact_tile(tl, th, d, stream_of_tile(d, n_streams, t), t, rec, grp);
         }
     }
@@ -2622,29 +2723,41 @@ int rc_launch_tiles(const KeyTables *d_tables, StreamDesc desc, uint64_t n_strea
     uint64_t grid = (n_tiles + waves_per_wg - 1) / waves_per_wg;
     const uint64_t cus = (uint64_t)cu_count();
     if (grid > cus) grid = cus;  // persistent: one 144 KiB-LDS workgroup per CU
-    // the tie lists: n_tiles slots, then one count per wave
-    uint32_t *d_xcount = d_xlist + n_tiles;
     const uint64_t n_waves = grid * waves_per_wg;
+    const TileUnits U = tile_units(n_tiles, n_waves);
+    // the tie lists: n_tiles slots, one count per unit, the grab counter
+    uint32_t *d_xcount = d_xlist + n_tiles;
+    uint32_t *d_ctr = d_xcount + U.n_units;
+    if (U.n_units > U.nw && hipMemsetAsync(d_ctr, 0, sizeof(uint32_t), st) != hipSuccess) {
+        snprintf(g_launch_err, sizeof g_launch_err, "hipMemsetAsync failed");
+        return 1;
+    }
     if (d_grp)
         hipLaunchKernelGGL(rc_tile_kernel<kTileGroups>, dim3((unsigned)grid), dim3(1024), 0, st,
-                           d_tables, desc, n_streams, n_tiles, d_records, d_grp, hot, d_xlist,
-                           d_xcount);
+                           d_tables, desc, n_streams, U, d_records, d_grp, hot, d_xlist,
+                           d_xcount, d_ctr);
     else
         hipLaunchKernelGGL(rc_tile_kernel<1>, dim3((unsigned)grid), dim3(1024), 0, st, d_tables,
-                           desc, n_streams, n_tiles, d_records, d_grp, hot, d_xlist, d_xcount);
+                           desc, n_streams, U, d_records, d_grp, hot, d_xlist, d_xcount, d_ctr);
     if (launch_status("rc_tile_kernel")) return 1;
     if (mid_event && hipEventRecord((hipEvent_t)mid_event, st) != hipSuccess) {
         snprintf(g_launch_err, sizeof g_launch_err, "hipEventRecord failed");
         return 1;
     }
     // one wave per tie list (almost always empty) and per host-listed tile, grid-strided
-    uint64_t egrid = (n_waves + 3) / 4;
+    uint64_t egrid = (U.n_units + 3) / 4;
     if (egrid > 4 * cus) egrid = 4 * cus;
     if (egrid == 0) egrid = 1;
     hipLaunchKernelGGL(rc_edge_kernel, dim3((unsigned)egrid), dim3(256), 0, st, d_tables, desc,
-                       n_streams, n_tiles, d_records, d_grp, (const uint32_t *)d_xlist,
-                       (const uint32_t *)d_xcount, n_waves);
+                       n_streams, U, d_records, d_grp, (const uint32_t *)d_xlist,
+                       (const uint32_t *)d_xcount);
     return launch_status("rc_edge_kernel");
+}
+
+uint64_t rc_tie_list_words(uint64_t n_tiles) {
+    // n_tiles list slots + one count per unit (static units: at most n_tiles + 15 waves;
+    // dynamic: at most n_tiles / kDynChunkMin + 1) + the grab counter
+    return 2 * n_tiles + n_tiles / kDynChunkMin + 64;
 }
 
 int rc_launch_chain(const KeyTables *d_tables, StreamDesc desc, uint64_t n_streams,
