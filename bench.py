@@ -829,6 +829,11 @@ def main(argv=None, backend=Backend):
             sample = min(args.cpu_streams or n, n)
             cpu, cpu_ends = cpu_baseline(sample, size, synth.DEFAULT_SEED, procs)
             cpu['affinity_cores'] = seen
+            cpu['cores_basis'] = (
+                f'{procs} = min(affinity mask {seen}, OMP_NUM_THREADS) -- the host-core share '
+                f'the GPU box grants each GPU (OMP_NUM_THREADS; nproc and the mask show the whole '
+                f"machine); --cpu-procs overrides" if os.environ.get('OMP_NUM_THREADS')
+                else f'{procs} = the affinity mask')
             if ends is not None:
                 cpu['matches_gpu'] = bool(all(np.array_equal(np.asarray(cpu_ends[i], np.uint64),
                                                              ends[i]) for i in cpu_ends))

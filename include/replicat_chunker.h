@@ -126,9 +126,10 @@ int rc_fill_splitmix_at(uint8_t *d_dst, uint64_t nbytes, uint64_t seed, uint64_t
                         uint64_t word0, void *hip_stream);
 
 /* Calibration (bench.py --calibrate): stream the first nbytes (whole 16 KiB tiles) of a
- * 16-byte aligned device buffer with the tile kernel's exact load pattern and no hashing; its
- * rate is the attainable streaming-read ceiling for the tile kernel on this device.
- * Enqueue only. */
+ * 16-byte aligned device buffer with the tile kernel's exact load pattern and work schedule
+ * (static ranges + grabbed units) and no hashing; its rate is the attainable streaming-read
+ * ceiling for the tile kernel on this device.  d_out: 4 u32 of device scratch (d_out[1] is the
+ * schedule's grab counter, zeroed by the call on its stream).  Enqueue only. */
 int rc_read_probe(const uint8_t *d_src, uint64_t nbytes, uint32_t *d_out, void *hip_stream);
 
 /* Keys j (key j covers bytes [4j-4, 4j+4)) that any argmax window of a stream (L, P) can
