@@ -551,12 +551,14 @@ __host__ inline TileUnits tile_units(uint64_t n_tiles, uint64_t nw) {
     TileUnits U;
     U.n_tiles = (uint32_t)n_tiles;
     U.nw = (uint32_t)nw;
-    uint64_t permille = 250, chunk = 32;
+    uint64_t permille = 250, chunk = 32, dyn_min = kDynMinPerWave;
     if (const char *e = getenv("RC_TILE_STATIC")) permille = strtoull(e, nullptr, 0);
     if (const char *e = getenv("RC_TILE_CHUNK")) chunk = strtoull(e, nullptr, 0);
+    // RC_TILE_DYN_MIN (tests): the tiles per wave from which units are dynamic
+    if (const char *e = getenv("RC_TILE_DYN_MIN")) dyn_min = strtoull(e, nullptr, 0);
     if (permille > 1000) permille = 1000;
     if (chunk < kDynChunkMin) chunk = kDynChunkMin;
-    if (n_tiles < kDynMinPerWave * nw || permille == 1000) {  // fully static
+    if (n_tiles < dyn_min * nw || permille == 1000) {  // fully static
         U.s0 = (uint32_t)((n_tiles + nw - 1) / nw);
         U.chunk = 1;
         U.dyn0 = (uint32_t)n_tiles;
@@ -861,32 +863,44 @@ __global__ __launch_bounds__(256) void rc_edge_kernel(const KeyTables *__restric
     const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
     const uint64_t n_host = sload(d.xtiles);
     const uint64_t n_units = U.n_units;
+    const uint64_t n_items = n_units + n_host;
+    const uint32_t lane = lane_id();
+    // Items (tie lists of the units, then the host's tiles) are the wave's gw, gw + nw, ...,
+    // looked at 64 at a time: lane l loads item e0 + l nw's count, one ballot says which have
+    // work (round 3: ~23 units per wave on config 2 -- one dependent load each was 10 us).
+    auto needs = [&](uint64_t e0) -> uint64_t {
+        const uint64_t e = e0 + lane * nw;
+        const bool w = e < n_items && (e >= n_units || xcount[e] != 0);
+        return __ballot(w);
+    };
     // almost every workgroup has nothing to recompute: it leaves before staging the tables
     bool work = false;
-    for (uint64_t e = gw; e < n_units + n_host && !work; e += nw)
-        work = e >= n_units || __builtin_amdgcn_readfirstlane(xcount[e]) != 0;
+    for (uint64_t e0 = gw; e0 < n_items && !work; e0 += 64 * nw) work = needs(e0) != 0;
     if (!__syncthreads_or(work)) return;
     const uint64_t *gfull = &tab->tl[0][0];
     for (uint32_t i = threadIdx.x; i < 2048u; i += blockDim.x) s_full[i] = gfull[i];
     __syncthreads();
     const uint64_t *tl = s_full, *th = s_full + 1024;
-    for (uint64_t e = gw; e < n_units + n_host; e += nw) {
-        if (e < n_units) {
-            uint32_t t0, t1;
-            U.range((uint32_t)e, t0, t1);
-            const uint32_t c = (uint32_t)__builtin_amdgcn_readfirstlane(xcount[e]);
-            for (uint32_t i = 0; i < c; ++i) {
-                const uint64_t t = (uint32_t)__builtin_amdgcn_readfirstlane(xlist[t0 + i]);
-                // the marker the tile kernel left: candidate lanes, ~stream
-                const uint64_t lanes = sload(&rec[t].key), s = ~sload(&rec[t].j) & 0x7fffffffu;
-                if (__builtin_popcountll(lanes) <= kTieLanes)
-                    exact_lanes(tl, th, d, s, t, lanes, rec);  // its group record stays valid
-                else  // e.g. constant data: every lane a candidate
-                    exact_tile(tl, th, d, s, t, rec, grp);
+    for (uint64_t e0 = gw; e0 < n_items; e0 += 64 * nw) {
+        for (uint64_t m = needs(e0); m; m &= m - 1) {
+            const uint64_t e = e0 + (uint64_t)__builtin_ctzll(m) * nw;
+            if (e < n_units) {
+                uint32_t t0, t1;
+                U.range((uint32_t)e, t0, t1);
+                const uint32_t c = (uint32_t)__builtin_amdgcn_readfirstlane(xcount[e]);
+                for (uint32_t i = 0; i < c; ++i) {
+                    const uint64_t t = (uint32_t)__builtin_amdgcn_readfirstlane(xlist[t0 + i]);
+                    // the marker the tile kernel left: candidate lanes, ~stream
+                    const uint64_t lanes = sload(&rec[t].key), s = ~sload(&rec[t].j) & 0x7fffffffu;
+                    if (__builtin_popcountll(lanes) <= kTieLanes)
+                        exact_lanes(tl, th, d, s, t, lanes, rec);  // its group record stays valid
+                    else  // e.g. constant data: every lane a candidate
+                        exact_tile(tl, th, d, s, t, rec, grp);
+                }
+            } else {
+                const uint64_t t = sload(d.xtiles + 1 + (e - n_units));
+                exact_tile(tl, th, d, stream_of_tile(d, n_streams, t), t, rec, grp);
             }
-        } else {
-            const uint64_t t = sload(d.xtiles + 1 + (e - n_units));
-            exact_tile(tl, th, d, stream_of_tile(d, n_streams, t), t, rec, grp);
         }
     }
 }

@@ -66,10 +66,22 @@ def main():
             if isinstance(d, dict) and 'FETCH_SIZE' in d:
                 d['hbm_read_bytes_calibrated'] = d['FETCH_SIZE'] * 1024 * factor
     out['workload'] = WORKLOAD
-    # the library build these counters are of (bench.py refuses a summary of another build)
-    sys.path.insert(0, ROOT)
-    from replicat_amd.build import embedded_id
-    out['build_id'] = embedded_id()
+    # the library build these counters are of (bench.py refuses a summary of another build):
+    # the build id the profiled bench command printed (its JSON line in trace.log); the local
+    # library's id only if that line is missing -- the tree may have been rebuilt since the run
+    bid = None
+    try:
+        for line in open(os.path.join(src, 'trace.log')):
+            if line.startswith('{'):
+                bid = json.loads(line).get('roofline', {}).get('build_id') or bid
+    except OSError:
+        pass
+    if bid is None:
+        sys.path.insert(0, ROOT)
+        from replicat_amd.build import embedded_id
+        bid = embedded_id()
+        print('warning: no bench line in trace.log; stamping the local library build', bid)
+    out['build_id'] = bid
     with open(os.path.join(dst, 'pmc_summary.json'), 'w') as f:
         json.dump(out, f, indent=1, sort_keys=True)
     print(json.dumps(out.get('rc_tile_kernel', {}), indent=1))

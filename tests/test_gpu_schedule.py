@@ -1,0 +1,91 @@
+"""The tile kernel's work schedule (kernels.hip TileUnits): static ranges, then units grabbed
+from a counter.  By default only launches of at least 128 tiles per wave (8 GiB on MI355X) use
+grabbed units, so the ordinary parity tests run most cases on the static path; here the same
+oracle checks run with RC_TILE_DYN_MIN=0 (every launch dynamic) and small units, so unit
+switches land everywhere: inside streams, on stream boundaries, on tiles the fast path does not
+take, on tie tiles (zeros: every tile ties), in segmented chains.  The schedule is read per
+launch (tile_units), so monkeypatch.setenv applies to the next call."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip('torch')
+if not torch.cuda.is_available():  # pragma: no cover - CPU container
+    pytest.skip('needs an MI355X', allow_module_level=True)
+
+import test_gpu_parity as P  # noqa: E402
+from gpu_util import chunk_device, device_streams  # noqa: E402
+
+from replicat_amd import synth  # noqa: E402
+from replicat_amd.chunker import GpuChunker  # noqa: E402
+
+SCHEDULES = [('0', '2'), ('250', '3'), ('900', '7'), ('0', '32')]
+
+
+@pytest.fixture(params=SCHEDULES, ids=['s%s_c%s' % x for x in SCHEDULES])
+def dynamic(request, monkeypatch):
+    st, ck = request.param
+    monkeypatch.setenv('RC_TILE_DYN_MIN', '0')
+    monkeypatch.setenv('RC_TILE_STATIC', st)
+    monkeypatch.setenv('RC_TILE_CHUNK', ck)
+    return request.param
+
+
+@pytest.mark.parametrize('seed', [0, 2, 5])
+def test_random_vs_oracle_dynamic(dynamic, seed):
+    P.test_random_vs_oracle(seed)
+
+
+@pytest.mark.parametrize('kind', ['random', 'zeros', 'periodic', 'framed'])
+def test_tile_records_dynamic(dynamic, kind):
+    P.test_tile_records_vs_oracle(kind)
+
+
+@pytest.mark.parametrize('kind', ['random', 'zeros'])
+def test_tile_group_maxima_dynamic(dynamic, kind):
+    P.test_tile_group_maxima_vs_oracle(kind)
+
+
+def test_segmented_chains_dynamic(dynamic, monkeypatch):
+    P.test_segmented_chains_vs_oracle(monkeypatch, 1 << 16, 1, '0')
+
+
+def test_many_small_streams_dynamic(dynamic):
+    """Units spanning many streams (the cursor re-seeks at every unit switch)."""
+    o = P._oracle()
+    mn, mx = 64, 4096
+    key = synth.seeded_key(21)
+    ch = GpuChunker(mn, mx, key)
+    rnd = np.random.default_rng(5)
+    sizes = [int(x) for x in rnd.integers(0, 70_000, 600)]
+    datas = [synth.stream_bytes(n, synth.DEFAULT_SEED, 900 + i) for i, n in enumerate(sizes)]
+    last = [int(rnd.integers(0, n + 1)) if n else 0 for n in sizes]
+    ts = device_streams(sizes, datas=datas)
+    got = chunk_device(ch, ts, sizes, last)
+    for d, L, g in zip(datas, last, got):
+        assert g == o.chunk_stream(d, mn, mx, key, L)
+
+
+def test_constant_data_default_schedule():
+    """8 GiB of zeros in one launch under the DEFAULT schedule (grabbed units): every tile is a
+    tie tile, resolved by the edge kernel from the per-unit lists; 16 identical streams, each
+    checked against the oracle's cut list of one of them."""
+    o = P._oracle()
+    n, size = 16, 512 << 20
+    ch = GpuChunker(128_000, 5_120_000, b'\xff' * 16)
+    pool = torch.zeros(n * size + 64, dtype=torch.uint8, device='cuda')
+    exp = o.chunk_stream(np.zeros(size, np.uint8), 128_000, 5_120_000, None, 0)
+    total, caps = ch.capacity([size] * n)
+    cuts = torch.zeros(total, dtype=torch.int64, device='cuda')
+    counts = torch.zeros(n, dtype=torch.int64, device='cuda')
+    ch.chunk_device([pool.data_ptr() + i * size for i in range(n)], [size] * n, None,
+                    cuts.data_ptr(), counts.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    c = cuts.cpu().numpy().view(np.uint64)
+    k = counts.cpu().numpy()
+    base = np.concatenate([[0], np.cumsum(caps)[:-1]]).astype(np.int64)
+    for i in range(n):
+        assert c[base[i]:base[i] + k[i]].tolist() == exp, i
+    del pool
+    torch.cuda.empty_cache()
