@@ -1576,7 +1576,12 @@ __global__ __launch_bounds__(kChainWaves * 64) void rc_spec_kernel(const KeyTabl
     const uint64_t s = find_index(d.seg_base, n_streams + 1, q);
     const uint64_t sb = sload(d.seg_base + s), nseg = sload(d.seg_base + s + 1) - sb;
     const uint64_t i = q - sb;
+#ifdef RC_DIAG_STAMPS
+    ChainStream st = chain_stream(d, s);
+    st.diag = st.diag && i == (nseg > 8 ? 7 : 0);  // one walker of stream 0 (a mid segment)
+#else
     const ChainStream st = chain_stream(d, s);
+#endif
     const bool direct = nseg == 1;
     uint64_t *out = direct ? cuts + sload(d.cut_base + s) : scratch + sload(d.scratch_base + s) + i * prm.seg_cap;
     const uint64_t cap = direct ? sload(d.cut_cap + s) : prm.seg_cap;

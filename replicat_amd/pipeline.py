@@ -274,11 +274,11 @@ class DeviceSnapshotProducer:
         if min_length > max_length:
             raise ValueError(f'Minimum length ({min_length}) is greater '
                              f'than the maximum one ({max_length})')
+        if int(slots) < 2:
+            raise ValueError('slots must be at least 2 (one batch filled while one is on the device)')
         self.device = int(device)
         self.dev = torch.device('cuda', self.device)
         self.chunker = GpuChunker(min_length, max_length, normalize_params(params), device=self.device)
-        if int(slots) < 2:
-            raise ValueError('slots must be at least 2 (one batch filled while one is on the device)')
         self.min_length, self.max_length = min_length, max_length
         self.digest_size = digest_size
         self.batch_bytes = max(int(batch_bytes), 2 * max_length + 16)

@@ -109,3 +109,11 @@ def test_pending_reports_a_failed_piece():
         pipeline._HostHash(Bad()).push(memoryview(b'x'), sl, pool)
         with pytest.raises(ValueError, match='boom'):
             sl.wait()
+
+
+@pytest.mark.parametrize('slots', [0, 1])
+def test_producer_needs_two_slots(slots):
+    """One batch is filled while another is on the device: fewer than two slots is refused
+    before anything touches a device."""
+    with pytest.raises(ValueError, match='slots'):
+        pipeline.DeviceSnapshotProducer(slots=slots, device=0)
