@@ -277,12 +277,181 @@ __device__ __forceinline__ void write_digest(uint8_t *slot, int q, uint64_t h0, 
 
 }  // namespace
 
+namespace {
+
+// ---- one LANE per chunk (round 3): the throughput form for many short chunks.
+//
+// A quad spends ~720 VALU per lane on a compression (2,880 lane-instructions per block, 20 %
+// of it the diagonal step's DPP moves); one lane holding the whole 16-word state needs ~1,900
+// and no cross-lane moves, so a batch of many short chunks -- where the VALU throughput, not one
+// chain, sets the time -- hashes ~1.5x faster this way.  A single chain is ~3x slower than a
+// quad's, so only chunks short enough to finish well inside the batch's time go to lanes
+// (lane_max_len, chosen by the host from the batch size).
+
+__device__ __forceinline__ void g_lane(uint64_t &a, uint64_t &b, uint64_t &c, uint64_t &d,
+                                       uint64_t x, uint64_t y) {
+    a = a + b + x;
+    d = rotr<32>(d ^ a);
+    c = c + d;
+    b = rotr<24>(b ^ c);
+    a = a + b + y;
+    d = rotr<16>(d ^ a);
+    c = c + d;
+    b = rotr<63>(b ^ c);
+}
+
+// RFC 7693 F: h ^= the 12-round mix of (h, IV ^ (t, 0, final, 0)) over message m.
+__device__ __forceinline__ void compress_lane(uint64_t (&h)[8], const uint64_t (&m)[16], uint64_t t,
+                                              bool final) {
+    uint64_t v[16];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        v[i] = h[i];
+        v[8 + i] = kIV[i];
+    }
+    v[12] ^= t;
+    if (final) v[14] = ~v[14];
+#pragma unroll
+    for (int r = 0; r < 12; ++r) {
+        const uint8_t *sg = kSigma[r % 10];
+        g_lane(v[0], v[4], v[8], v[12], m[sg[0]], m[sg[1]]);
+        g_lane(v[1], v[5], v[9], v[13], m[sg[2]], m[sg[3]]);
+        g_lane(v[2], v[6], v[10], v[14], m[sg[4]], m[sg[5]]);
+        g_lane(v[3], v[7], v[11], v[15], m[sg[6]], m[sg[7]]);
+        g_lane(v[0], v[5], v[10], v[15], m[sg[8]], m[sg[9]]);
+        g_lane(v[1], v[6], v[11], v[12], m[sg[10]], m[sg[11]]);
+        g_lane(v[2], v[7], v[8], v[13], m[sg[12]], m[sg[13]]);
+        g_lane(v[3], v[4], v[9], v[14], m[sg[14]], m[sg[15]]);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) h[i] ^= v[i] ^ v[8 + i];
+}
+
+struct LaneRaw {  // 132 bytes from a 4-aligned address: one block plus the funnel spill
+    u32x4 q[8];
+    uint32_t z;
+};
+
+__device__ __forceinline__ LaneRaw lane_load(gbytes a4) {
+    LaneRaw r;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r.q[i] = *reinterpret_cast<const GLOBAL u32x4 *>(a4 + 16 * i);
+    r.z = *reinterpret_cast<const GLOBAL uint32_t *>(a4 + 128);
+    return r;
+}
+
+// the block's 16 little-endian words, funnelled by sh bytes (a no-op shift when aligned)
+__device__ __forceinline__ void lane_words(const LaneRaw &r, uint32_t sh, uint64_t (&m)[16]) {
+    const uint32_t sb = sh * 8;
+    uint32_t w[33];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        w[4 * i] = r.q[i].x;
+        w[4 * i + 1] = r.q[i].y;
+        w[4 * i + 2] = r.q[i].z;
+        w[4 * i + 3] = r.q[i].w;
+    }
+    w[32] = r.z;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const uint32_t lo = __builtin_amdgcn_alignbit(w[2 * i + 1], w[2 * i], sb);
+        const uint32_t hi = __builtin_amdgcn_alignbit(w[2 * i + 2], w[2 * i + 1], sb);
+        m[i] = (uint64_t(hi) << 32) | lo;
+    }
+}
+
+// hash_digest of one message (len bytes at p) by one lane into out (outlen bytes of 64, the
+// rest zero).  Nothing beyond the message's last dword is read.
+__device__ __forceinline__ void lane_hash(gbytes p, uint64_t len, uint32_t outlen, uint8_t *out) {
+    uint64_t h[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) h[i] = kIV[i];
+    h[0] ^= 0x01010000ull | outlen;
+    const uint64_t nfull = len ? (len - 1) / 128 : 0;  // non-final blocks
+    const uint32_t sh = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(p) & 3);
+    gbytes a4 = p - sh;
+    uint64_t m[16];
+    if (nfull) {
+        LaneRaw nxt = lane_load(a4);
+#pragma unroll 1
+        for (uint64_t b = 0; b < nfull; ++b) {
+            const LaneRaw cur = nxt;
+            // the next block's loads go out before this block's compression; the last full
+            // block re-reads itself (always readable) so every iteration issues the same loads
+            nxt = lane_load(a4 + 128 * (b + 1 < nfull ? b + 1 : b));
+            lane_words(cur, sh, m);
+            compress_lane(h, m, 128 * (b + 1), false);
+        }
+    }
+    // the last 1..128 bytes (none for an empty message), zero past the end
+    const int64_t rem = static_cast<int64_t>(len - nfull * 128);
+    uint32_t w[33];
+    if (len) {
+        const uintptr_t last = (reinterpret_cast<uintptr_t>(p) + len - 1) & ~uintptr_t(3);
+        const uintptr_t f4 = reinterpret_cast<uintptr_t>(a4) + 128 * nfull;
+#pragma unroll
+        for (int i = 0; i < 33; ++i) {
+            uintptr_t a = f4 + 4 * i;
+            a = a < last ? a : last;
+            w[i] = *reinterpret_cast<const GLOBAL uint32_t *>(a);
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 33; ++i) w[i] = 0;
+    }
+    {
+        const uint32_t sb = sh * 8;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const uint32_t lo = __builtin_amdgcn_alignbit(w[2 * i + 1], w[2 * i], sb) & byte_mask(rem - 8 * i);
+            const uint32_t hi = __builtin_amdgcn_alignbit(w[2 * i + 2], w[2 * i + 1], sb) &
+                                byte_mask(rem - 8 * i - 4);
+            m[i] = (uint64_t(hi) << 32) | lo;
+        }
+    }
+    compress_lane(h, m, len, true);
+    uint64_t *o = reinterpret_cast<uint64_t *>(out);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int v = static_cast<int>(outlen) - 8 * i;
+        o[i] = v >= 8 ? h[i] : v <= 0 ? 0ull : h[i] & ((1ull << (8 * v)) - 1);
+    }
+}
+
+// first index of the longest-first list whose length is at most lane_max (binary search)
+__device__ __forceinline__ uint64_t lane_split(const B2Item *items, uint64_t total, uint64_t lane_max) {
+    uint64_t lo = 0, hi = total;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (items[mid].len <= lane_max) hi = mid;
+        else lo = mid + 1;
+    }
+    return lo;
+}
+
+}  // namespace
+
 // One quad per chunk; a workgroup is kB2Threads / 4 quads.  Items g = quad, quad + Q, ...
+// Workgroups [0, quad_groups) hash the list's items [0, k) by quads; the rest hash items
+// [k, total) one per lane, where k is the first item of at most lane_max bytes (the list is
+// longest first; lane_max 0: every item by quads).
 __global__ __launch_bounds__(kB2Threads) void rc_b2_kernel(const B2Item *__restrict__ items,
                                                            const uint64_t *__restrict__ d_total,
                                                            uint64_t n_static, uint32_t outlen,
-                                                           uint8_t *__restrict__ out) {
+                                                           uint8_t *__restrict__ out,
+                                                           uint64_t lane_max, uint32_t quad_groups) {
     __shared__ uint64_t blocks[kB2Threads / 4 * 16];
+    const uint64_t all = d_total ? *d_total : n_static;
+    const uint64_t k = lane_max ? lane_split(items, all, lane_max) : all;
+    if (blockIdx.x >= quad_groups) {  // lane role: items k + i, k + i + NL, ..
+        const uint64_t nl = uint64_t(gridDim.x - quad_groups) * kB2Threads;
+        for (uint64_t g = k + uint64_t(blockIdx.x - quad_groups) * kB2Threads + threadIdx.x; g < all;
+             g += nl) {
+            const B2Item it = items[g];
+            lane_hash(reinterpret_cast<gbytes>(it.ptr), it.len, outlen, out + it.slot * kB2Slot);
+        }
+        return;
+    }
     const int q = threadIdx.x & 3;
     const int quad = threadIdx.x >> 2;
     uint64_t *qb = blocks + quad * 16;
@@ -294,10 +463,10 @@ __global__ __launch_bounds__(kB2Threads) void rc_b2_kernel(const B2Item *__restr
     // One wave per SIMD (256 groups) unless items are plentiful: a BLAKE2b compression is
     // VALU-issue bound, so a second wave on a SIMD halves the speed of the first -- and the
     // longest chunk's wave sets the end of the launch.  Every group computes the same count.
-    const uint64_t total = d_total ? *d_total : n_static;
+    const uint64_t total = k;
     const uint64_t per_group = kB2Threads / 4;
     uint64_t groups = total >= kB2TwoWaveItems ? kB2MaxGroups : kB2OneWaveGroups;
-    groups = groups < gridDim.x ? groups : gridDim.x;
+    groups = groups < quad_groups ? groups : quad_groups;
     const uint64_t need = (total + per_group - 1) / per_group;
     groups = need < groups ? (need ? need : 1) : groups;
     if (blockIdx.x >= groups) return;
@@ -566,17 +735,27 @@ unsigned b2_grid(uint64_t upper) {
 
 const char *rc_b2_launch_error(void) { return g_b2_err; }
 
+// lane-role workgroups for up to `upper` items: two waves per SIMD at most (kB2MaxGroups)
+static unsigned b2_lane_grid(uint64_t upper, uint64_t lane_max) {
+    if (!lane_max) return 0;
+    uint64_t wg = (upper + kB2Threads - 1) / kB2Threads;
+    if (wg > kB2MaxGroups) wg = kB2MaxGroups;
+    return static_cast<unsigned>(wg);
+}
+
 int rc_b2_launch_items(const B2Item *d_items, uint64_t n, uint32_t outlen, uint8_t *d_out,
-                       hipStream_t stream) {
+                       uint64_t lane_max, hipStream_t stream) {
     if (!n) return 0;
-    rc_b2_kernel<<<b2_grid(n), kB2Threads, 0, stream>>>(d_items, nullptr, n, outlen, d_out);
+    const unsigned qg = b2_grid(n);
+    rc_b2_kernel<<<qg + b2_lane_grid(n, lane_max), kB2Threads, 0, stream>>>(d_items, nullptr, n, outlen,
+                                                                          d_out, lane_max, qg);
     return b2_status("rc_b2_kernel");
 }
 
 int rc_b2_launch_chunks(uint64_t n, const uint64_t *d_ptrs, const uint64_t *d_cut_base,
                         const uint64_t *d_cuts, const int64_t *d_counts, uint64_t *d_chunk_off,
                         uint32_t *d_hist, B2Item *d_items, uint64_t items_cap, uint32_t outlen,
-                        uint8_t *d_out, hipStream_t stream) {
+                        uint8_t *d_out, uint64_t lane_max, hipStream_t stream) {
     if (!n) return 0;
     rc_b2_scan_kernel<<<1, 1024, 0, stream>>>(d_counts, n, d_chunk_off);
     if (b2_status("rc_b2_scan_kernel")) return 1;
@@ -588,8 +767,9 @@ int rc_b2_launch_chunks(uint64_t n, const uint64_t *d_ptrs, const uint64_t *d_cu
     if (b2_status("rc_b2_hscan_kernel")) return 1;
     rc_b2_scatter_kernel<<<groups, 256, 0, stream>>>(c, d_hist, d_items);
     if (b2_status("rc_b2_scatter_kernel")) return 1;
-    rc_b2_kernel<<<b2_grid(items_cap), kB2Threads, 0, stream>>>(d_items, d_chunk_off + n, 0,
-                                                                outlen, d_out);
+    const unsigned qg = b2_grid(items_cap);
+    rc_b2_kernel<<<qg + b2_lane_grid(items_cap, lane_max), kB2Threads, 0, stream>>>(
+        d_items, d_chunk_off + n, 0, outlen, d_out, lane_max, qg);
     return b2_status("rc_b2_kernel");
 }
 

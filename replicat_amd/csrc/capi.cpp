@@ -797,8 +797,13 @@ int chunk_host_impl(rc_chunker *ch, rc_hasher *hasher, uint64_t n, const uint8_t
             uint8_t *dd = static_cast<uint8_t *>(ch->d_hdig[slot].p);
             std::vector<uint64_t> cb(nb);
             for (uint64_t k = 0; k < nb; ++k) cb[k] = cut_base[i + k] - cut_base[i];
+            uint64_t bytes = 0, longest = 0;
+            for (uint64_t k = 0; k < nb; ++k) {
+                bytes += lens[i + k];
+                longest = std::max(longest, lens[i + k]);
+            }
             if (int rc = rc_hasher_enqueue_chunks(hasher, nb, dptr.data(), cb.data(), dc, dn, ncut,
-                                                  dd, st))
+                                                  bytes, std::min(longest, ch->max_length), dd, st))
                 return rc;
             HIP_TRY(hipMemcpyAsync(digests + cut_base[i] * kDigestSlot, dd, ncut * kDigestSlot,
                                    hipMemcpyDeviceToHost, st));

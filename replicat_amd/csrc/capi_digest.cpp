@@ -153,7 +153,10 @@ int enqueue_items(rc_hasher *h, uint64_t n, const uint8_t *const *d_ptrs, const 
     RC_HIP_TRY(hipMemcpyAsync(w->d_stage.p, w->h_stage.p, bytes, hipMemcpyHostToDevice, st));
     std::array<hipEvent_t, 2> ev{};
     if (int rc = timing_begin(h, st, ev)) return rc;
-    if (rc_b2_launch_items(static_cast<const B2Item *>(w->d_stage.p), n, h->digest_size, d_out, st))
+    uint64_t msg_bytes = 0;
+    for (uint64_t i = 0; i < n; ++i) msg_bytes += lens[i];
+    if (rc_b2_launch_items(static_cast<const B2Item *>(w->d_stage.p), n, h->digest_size, d_out,
+                           rc_b2_lane_max(msg_bytes, it[0].len), st))
         return rc_fail(RC_ERR_HIP, "%s", rc_b2_launch_error());
     if (int rc = timing_end(h, st, ev)) return rc;
     return finish(h, *w, st);
@@ -194,8 +197,8 @@ int check_buffers(uint64_t n, const uint8_t *const *ptrs, const uint64_t *lens) 
 
 int rc_hasher_enqueue_chunks(rc_hasher *h, uint64_t n, const uint8_t *const *d_ptrs,
                              const uint64_t *cut_base, const uint64_t *d_cuts,
-                             const int64_t *d_counts, uint64_t total_cap, uint8_t *d_out,
-                             hipStream_t st) {
+                             const int64_t *d_counts, uint64_t total_cap, uint64_t bytes,
+                             uint64_t longest, uint8_t *d_out, hipStream_t st) {
     if (!n) return 0;
     std::lock_guard<std::mutex> lock(h->mu);
     Guard g(h->device);
@@ -220,7 +223,7 @@ int rc_hasher_enqueue_chunks(rc_hasher *h, uint64_t n, const uint8_t *const *d_p
     uint32_t *hist = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(w->d_stage.p) + hist_off);
     if (rc_b2_launch_chunks(n, d, d + n, d_cuts, d_counts, chunk_off, hist,
                             static_cast<B2Item *>(w->d_items.p), total_cap, h->digest_size, d_out,
-                            st))
+                            rc_b2_lane_max(bytes, longest), st))
         return rc_fail(RC_ERR_HIP, "%s", rc_b2_launch_error());
     if (int rc = timing_end(h, st, ev)) return rc;
     return finish(h, *w, st);
@@ -326,8 +329,14 @@ int rc_blake2b_chunks(rc_hasher *h, const rc_chunker *layout, uint64_t n,
         base[i] = acc;
         acc += caps[i];
     }
-    return rc_hasher_enqueue_chunks(h, n, d_streams, base.data(), d_cuts, d_counts, total, d_digests,
-                                    static_cast<hipStream_t>(hip_stream));
+    uint64_t bytes = 0, longest = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        bytes += lens[i];
+        longest = std::max(longest, lens[i]);
+    }
+    if (const uint64_t m = rc_chunker_max_length(layout)) longest = std::min(longest, m);
+    return rc_hasher_enqueue_chunks(h, n, d_streams, base.data(), d_cuts, d_counts, total, bytes,
+                                    longest, d_digests, static_cast<hipStream_t>(hip_stream));
 }
 
 int rc_blake2b_state_init(uint32_t digest_size, const uint8_t *key, uint32_t keylen,

@@ -17,8 +17,10 @@ int rc_fail(int code, const char *fmt, ...);
 
 // Enqueue on `st` the digests of the chunks of n device streams (d_ptrs: HOST array of device
 // pointers) whose cut lists sit at d_cuts[cut_base[i] ..] with d_counts[i] entries, into
-// d_out + 64 * (cut_base[i] + k).  total_cap = sum of the cut capacities (>= the chunk count).
+// d_out + 64 * (cut_base[i] + k).  total_cap = sum of the cut capacities (>= the chunk count);
+// bytes = the streams' total length, longest = a bound on one chunk's length (they set the
+// lane / quad split, rc_b2_lane_max).
 int rc_hasher_enqueue_chunks(rc_hasher *h, uint64_t n, const uint8_t *const *d_ptrs,
                              const uint64_t *cut_base, const uint64_t *d_cuts,
-                             const int64_t *d_counts, uint64_t total_cap, uint8_t *d_out,
-                             hipStream_t st);
+                             const int64_t *d_counts, uint64_t total_cap, uint64_t bytes,
+                             uint64_t longest, uint8_t *d_out, hipStream_t st);

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/replicat_digest.h"
 
@@ -26,8 +27,10 @@ constexpr uint64_t kB2Slot = 64;      // bytes per digest slot (BLAKE2b's larges
 const char *rc_b2_launch_error(void);
 
 // Digests of n items (host-built work list, already on the device).
+// lane_max: items of at most this many bytes are hashed one per lane, longer ones by quads
+// (rc_b2_lane_max); 0: every item by quads.
 int rc_b2_launch_items(const B2Item *d_items, uint64_t n, uint32_t outlen, uint8_t *d_out,
-                       hipStream_t stream);
+                       uint64_t lane_max, hipStream_t stream);
 
 // Incremental updates of n (state, buffer) items; finals write the digest at d_out + 64 * slot.
 int rc_b2_launch_update(const B2UItem *d_items, uint64_t n, uint8_t *d_out, hipStream_t stream);
@@ -45,7 +48,19 @@ inline uint64_t rc_b2_hist_words(uint64_t n) {
 int rc_b2_launch_chunks(uint64_t n, const uint64_t *d_ptrs, const uint64_t *d_cut_base,
                         const uint64_t *d_cuts, const int64_t *d_counts, uint64_t *d_chunk_off,
                         uint32_t *d_hist, B2Item *d_items, uint64_t items_cap, uint32_t outlen,
-                        uint8_t *d_out, hipStream_t stream);
+                        uint8_t *d_out, uint64_t lane_max, hipStream_t stream);
+
+// The lane/quad split for a batch of `bytes` message bytes whose longest message is at most
+// `longest` bytes.  Lanes pay off only when the batch is throughput-bound: its ALU time
+// (~bytes / 1.7 TB/s) well above the longest quad chain (~longest / 128 x 1.4 us), i.e.
+// bytes >= longest << 16; otherwise every item goes to quads (config 2: its 5 MB chunks' chains
+// set the time, and lanes sharing their SIMDs only lengthen them).  Within a throughput-bound
+// batch a message goes to a lane when its chain (~3x a quad's) ends well inside the batch time:
+// len <= bytes >> 17.  RC_B2_LANE_MAX (bytes) overrides the whole rule, 0 turning lanes off.
+inline uint64_t rc_b2_lane_max(uint64_t bytes, uint64_t longest) {
+    if (const char *e = getenv("RC_B2_LANE_MAX")) return strtoull(e, nullptr, 0);
+    return longest > (bytes >> 16) ? 0 : bytes >> 17;
+}
 
 // Exclusive prefix of the per-stream chunk counts into d_chunk_off[0..n] (the total at [n]).
 int rc_b2_launch_scan(const int64_t *d_counts, uint64_t n, uint64_t *d_chunk_off, hipStream_t stream);
