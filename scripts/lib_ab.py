@@ -5,7 +5,7 @@ own chunker, and the builds take turns chunking the same device arena, round aft
 comparison.  Every build must produce the same cut lists (except the RC_DIAG_NO_TAIL
 diagnostic build, diag/lib_NOTAIL.so, which stores no records and is timed only).
 
-    python scripts/lib_ab.py [config] [rounds] LIB [LIB ...]      config: 2 | 3iii | 4 | harness
+    python scripts/lib_ab.py [config] [rounds] LIB [LIB ...]      config: 2 | 3ii | 3iii | 4 | harness
 """
 import ctypes
 import json
@@ -48,6 +48,7 @@ if cfg == 'harness':
 else:
     n, size, mn, mx = {'2': (1024, 64 << 20, 128_000, 5_120_000),
                        '3iii': (65536, 1 << 20, 2_000, 80_000),
+                       '3ii': (1, 64 << 30, 128_000, 5_120_000),
                        '4': (16, 8 << 30, 128_000, 5_120_000)}[cfg]
     pool = torch.empty(n * size + 64, dtype=torch.uint8, device='cuda')
     fill_splitmix_streams(pool.data_ptr(), n, size, size, synth.DEFAULT_SEED, 0, 1, hs)
