@@ -284,9 +284,9 @@ namespace {
 // A quad spends ~720 VALU per lane on a compression (2,880 lane-instructions per block, 20 %
 // of it the diagonal step's DPP moves); one lane holding the whole 16-word state needs ~1,900
 // and no cross-lane moves, so a batch of many short chunks -- where the VALU throughput, not one
-// chain, sets the time -- hashes ~1.5x faster this way.  A single chain is ~3x slower than a
-// quad's, so only chunks short enough to finish well inside the batch's time go to lanes
-// (lane_max_len, chosen by the host from the batch size).
+// chain, sets the time -- hashes faster this way (config 3 iii's 1.45 M chunks: 46.3 -> 37.7 ms).
+// A single chain is ~3x slower than a quad's, so only chunks short enough to finish well inside
+// the batch's time go to lanes (lane_max, rc_b2_lane_max in digest_kernels.h).
 
 __device__ __forceinline__ void g_lane(uint64_t &a, uint64_t &b, uint64_t &c, uint64_t &d,
                                        uint64_t x, uint64_t y) {
@@ -429,7 +429,31 @@ __device__ __forceinline__ uint64_t lane_split(const B2Item *items, uint64_t tot
     return lo;
 }
 
+// Items [first, all) one per lane, dealt round-robin over the lanes of `groups` workgroups
+// (this one is `group`): neighbouring lanes take neighbouring items of the longest-first list.
+__device__ __forceinline__ void lane_items(const B2Item *items, uint64_t first, uint64_t all,
+                                           uint64_t group, uint64_t groups, uint32_t outlen,
+                                           uint8_t *out) {
+    const uint64_t nl = groups * kB2Threads;
+    for (uint64_t g = first + group * kB2Threads + threadIdx.x; g < all; g += nl) {
+        const B2Item it = items[g];
+        lane_hash(reinterpret_cast<gbytes>(it.ptr), it.len, outlen, out + it.slot * kB2Slot);
+    }
+}
+
 }  // namespace
+
+// Every item one per lane: the launch for batches whose items are all short enough for lanes
+// (rc_b2_lane_max).  It holds 114 VGPRs against the quad kernel's 238, so four waves share a
+// SIMD instead of two -- the lane form is VALU-throughput bound, and one wave issues a VALU
+// instruction only every ~5-6 cycles.
+__global__ __launch_bounds__(kB2Threads) void rc_b2_lane_kernel(const B2Item *__restrict__ items,
+                                                                const uint64_t *__restrict__ d_total,
+                                                                uint64_t n_static, uint32_t outlen,
+                                                                uint8_t *__restrict__ out) {
+    const uint64_t all = d_total ? *d_total : n_static;
+    lane_items(items, 0, all, blockIdx.x, gridDim.x, outlen, out);
+}
 
 // One quad per chunk; a workgroup is kB2Threads / 4 quads.  Items g = quad, quad + Q, ...
 // Workgroups [0, quad_groups) hash the list's items [0, k) by quads; the rest hash items
@@ -444,12 +468,7 @@ __global__ __launch_bounds__(kB2Threads) void rc_b2_kernel(const B2Item *__restr
     const uint64_t all = d_total ? *d_total : n_static;
     const uint64_t k = lane_max ? lane_split(items, all, lane_max) : all;
     if (blockIdx.x >= quad_groups) {  // lane role: items k + i, k + i + NL, ..
-        const uint64_t nl = uint64_t(gridDim.x - quad_groups) * kB2Threads;
-        for (uint64_t g = k + uint64_t(blockIdx.x - quad_groups) * kB2Threads + threadIdx.x; g < all;
-             g += nl) {
-            const B2Item it = items[g];
-            lane_hash(reinterpret_cast<gbytes>(it.ptr), it.len, outlen, out + it.slot * kB2Slot);
-        }
+        lane_items(items, k, all, blockIdx.x - quad_groups, gridDim.x - quad_groups, outlen, out);
         return;
     }
     const int q = threadIdx.x & 3;
@@ -743,9 +762,21 @@ static unsigned b2_lane_grid(uint64_t upper, uint64_t lane_max) {
     return static_cast<unsigned>(wg);
 }
 
+// lane-only workgroups for up to `upper` items: four waves per SIMD at most
+static unsigned b2_lane_only_grid(uint64_t upper) {
+    uint64_t wg = (upper + kB2Threads - 1) / kB2Threads;
+    if (wg > kB2LaneGroups) wg = kB2LaneGroups;
+    return static_cast<unsigned>(wg ? wg : 1);
+}
+
 int rc_b2_launch_items(const B2Item *d_items, uint64_t n, uint32_t outlen, uint8_t *d_out,
-                       uint64_t lane_max, hipStream_t stream) {
+                       uint64_t lane_max, bool lane_only, hipStream_t stream) {
     if (!n) return 0;
+    if (lane_only) {
+        rc_b2_lane_kernel<<<b2_lane_only_grid(n), kB2Threads, 0, stream>>>(d_items, nullptr, n,
+                                                                           outlen, d_out);
+        return b2_status("rc_b2_lane_kernel");
+    }
     const unsigned qg = b2_grid(n);
     rc_b2_kernel<<<qg + b2_lane_grid(n, lane_max), kB2Threads, 0, stream>>>(d_items, nullptr, n, outlen,
                                                                           d_out, lane_max, qg);
@@ -755,7 +786,7 @@ int rc_b2_launch_items(const B2Item *d_items, uint64_t n, uint32_t outlen, uint8
 int rc_b2_launch_chunks(uint64_t n, const uint64_t *d_ptrs, const uint64_t *d_cut_base,
                         const uint64_t *d_cuts, const int64_t *d_counts, uint64_t *d_chunk_off,
                         uint32_t *d_hist, B2Item *d_items, uint64_t items_cap, uint32_t outlen,
-                        uint8_t *d_out, uint64_t lane_max, hipStream_t stream) {
+                        uint8_t *d_out, uint64_t lane_max, bool lane_only, hipStream_t stream) {
     if (!n) return 0;
     rc_b2_scan_kernel<<<1, 1024, 0, stream>>>(d_counts, n, d_chunk_off);
     if (b2_status("rc_b2_scan_kernel")) return 1;
@@ -767,6 +798,11 @@ int rc_b2_launch_chunks(uint64_t n, const uint64_t *d_ptrs, const uint64_t *d_cu
     if (b2_status("rc_b2_hscan_kernel")) return 1;
     rc_b2_scatter_kernel<<<groups, 256, 0, stream>>>(c, d_hist, d_items);
     if (b2_status("rc_b2_scatter_kernel")) return 1;
+    if (lane_only) {
+        rc_b2_lane_kernel<<<b2_lane_only_grid(items_cap), kB2Threads, 0, stream>>>(
+            d_items, d_chunk_off + n, 0, outlen, d_out);
+        return b2_status("rc_b2_lane_kernel");
+    }
     const unsigned qg = b2_grid(items_cap);
     rc_b2_kernel<<<qg + b2_lane_grid(items_cap, lane_max), kB2Threads, 0, stream>>>(
         d_items, d_chunk_off + n, 0, outlen, d_out, lane_max, qg);

@@ -155,8 +155,9 @@ int enqueue_items(rc_hasher *h, uint64_t n, const uint8_t *const *d_ptrs, const 
     if (int rc = timing_begin(h, st, ev)) return rc;
     uint64_t msg_bytes = 0;
     for (uint64_t i = 0; i < n; ++i) msg_bytes += lens[i];
+    const uint64_t lane_max = rc_b2_lane_max(msg_bytes, it[0].len);
     if (rc_b2_launch_items(static_cast<const B2Item *>(w->d_stage.p), n, h->digest_size, d_out,
-                           rc_b2_lane_max(msg_bytes, it[0].len), st))
+                           lane_max, rc_b2_lane_only(lane_max, it[0].len), st))
         return rc_fail(RC_ERR_HIP, "%s", rc_b2_launch_error());
     if (int rc = timing_end(h, st, ev)) return rc;
     return finish(h, *w, st);
@@ -221,9 +222,10 @@ int rc_hasher_enqueue_chunks(rc_hasher *h, uint64_t n, const uint8_t *const *d_p
     std::array<hipEvent_t, 2> ev{};
     if (int rc = timing_begin(h, st, ev)) return rc;
     uint32_t *hist = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(w->d_stage.p) + hist_off);
+    const uint64_t lane_max = rc_b2_lane_max(bytes, longest);
     if (rc_b2_launch_chunks(n, d, d + n, d_cuts, d_counts, chunk_off, hist,
                             static_cast<B2Item *>(w->d_items.p), total_cap, h->digest_size, d_out,
-                            rc_b2_lane_max(bytes, longest), st))
+                            lane_max, rc_b2_lane_only(lane_max, longest), st))
         return rc_fail(RC_ERR_HIP, "%s", rc_b2_launch_error());
     if (int rc = timing_end(h, st, ev)) return rc;
     return finish(h, *w, st);

@@ -21,6 +21,7 @@ constexpr int kB2Threads = 256;       // 4 waves, 64 quads per workgroup
 constexpr uint64_t kB2MaxGroups = 512;  // 2 waves per SIMD on 256 CUs; items beyond loop
 constexpr uint64_t kB2OneWaveGroups = 256;   // one wave per SIMD
 constexpr uint64_t kB2TwoWaveItems = 65536;  // from this many items on, two waves per SIMD
+constexpr uint64_t kB2LaneGroups = 1024;     // lane-only launches: four waves per SIMD
 constexpr int kB2Buckets = 256;       // length classes of the longest-first work list
 constexpr uint64_t kB2Slot = 64;      // bytes per digest slot (BLAKE2b's largest digest)
 
@@ -28,9 +29,10 @@ const char *rc_b2_launch_error(void);
 
 // Digests of n items (host-built work list, already on the device).
 // lane_max: items of at most this many bytes are hashed one per lane, longer ones by quads
-// (rc_b2_lane_max); 0: every item by quads.
+// (rc_b2_lane_max); 0: every item by quads.  lane_only: every item by lanes, in the lane
+// kernel (four waves per SIMD) -- for batches whose items are all at most lane_max bytes.
 int rc_b2_launch_items(const B2Item *d_items, uint64_t n, uint32_t outlen, uint8_t *d_out,
-                       uint64_t lane_max, hipStream_t stream);
+                       uint64_t lane_max, bool lane_only, hipStream_t stream);
 
 // Incremental updates of n (state, buffer) items; finals write the digest at d_out + 64 * slot.
 int rc_b2_launch_update(const B2UItem *d_items, uint64_t n, uint8_t *d_out, hipStream_t stream);
@@ -48,7 +50,7 @@ inline uint64_t rc_b2_hist_words(uint64_t n) {
 int rc_b2_launch_chunks(uint64_t n, const uint64_t *d_ptrs, const uint64_t *d_cut_base,
                         const uint64_t *d_cuts, const int64_t *d_counts, uint64_t *d_chunk_off,
                         uint32_t *d_hist, B2Item *d_items, uint64_t items_cap, uint32_t outlen,
-                        uint8_t *d_out, uint64_t lane_max, hipStream_t stream);
+                        uint8_t *d_out, uint64_t lane_max, bool lane_only, hipStream_t stream);
 
 // The lane/quad split for a batch of `bytes` message bytes whose longest message is at most
 // `longest` bytes.  Lanes pay off only when the batch is throughput-bound: its ALU time
@@ -60,6 +62,13 @@ int rc_b2_launch_chunks(uint64_t n, const uint64_t *d_ptrs, const uint64_t *d_cu
 inline uint64_t rc_b2_lane_max(uint64_t bytes, uint64_t longest) {
     if (const char *e = getenv("RC_B2_LANE_MAX")) return strtoull(e, nullptr, 0);
     return longest > (bytes >> 16) ? 0 : bytes >> 17;
+}
+// Whether a batch whose messages are at most `longest` bytes goes to the lane kernel alone
+// (RC_B2_LANE_ONLY=0: never -- the fused kernel's lane role instead, for A/B runs).
+inline bool rc_b2_lane_only(uint64_t lane_max, uint64_t longest) {
+    if (const char *e = getenv("RC_B2_LANE_ONLY"))
+        if (e[0] == '0') return false;
+    return lane_max != 0 && longest <= lane_max;
 }
 
 // Exclusive prefix of the per-stream chunk counts into d_chunk_off[0..n] (the total at [n]).

@@ -1,8 +1,8 @@
-"""The one-lane-per-chunk form of the BLAKE2b digest kernel (blake2b.hip lane_hash): the same
-hashlib checks as tests/test_gpu_digest.py with the lane / quad split forced through
-RC_B2_LANE_MAX (read per call): every item by lanes, a mixed split, and the default split on a
-batch of many short chunks (config 3 iii's parameters), where most chunks take lanes.  Kernel
-ids: rc_b2_kernel's lane role, blake2b.hip lane_hash."""
+"""The one-lane-per-chunk form of the BLAKE2b digests (blake2b.hip lane_hash): the same hashlib
+checks as tests/test_gpu_digest.py with the lane / quad split forced through RC_B2_LANE_MAX and
+RC_B2_LANE_ONLY (read per call): every item by the lane kernel (rc_b2_lane_kernel), every item by
+the fused kernel's lane role (rc_b2_kernel), a mixed split, and the default split on batches of
+many short chunks (config 3 iii's parameters): a mixed one and a lane-only one."""
 
 import pytest
 
@@ -18,12 +18,17 @@ from replicat_amd import synth  # noqa: E402
 from replicat_amd.chunker import GpuChunker  # noqa: E402
 from replicat_amd.hashing import GpuBlake2b  # noqa: E402
 
-SPLITS = {'all_lanes': str(1 << 40), 'mixed': '3000'}
+# (RC_B2_LANE_MAX, RC_B2_LANE_ONLY): every item by the lane kernel; every item by the fused
+# kernel's lane role; the fused kernel with quads above 3,000 bytes and lanes below
+SPLITS = {'all_lanes': (str(1 << 40), '1'), 'all_lanes_fused': (str(1 << 40), '0'),
+          'mixed': ('3000', '1')}
 
 
 @pytest.fixture(params=sorted(SPLITS))
 def split(request, monkeypatch):
-    monkeypatch.setenv('RC_B2_LANE_MAX', SPLITS[request.param])
+    lane_max, lane_only = SPLITS[request.param]
+    monkeypatch.setenv('RC_B2_LANE_MAX', lane_max)
+    monkeypatch.setenv('RC_B2_LANE_ONLY', lane_only)
     return request.param
 
 
@@ -58,16 +63,19 @@ def test_chunk_digests_lanes(split, hasher, mn, mx):
     D.test_chunk_digests_match_hashlib(hasher, mn, mx)
 
 
-def test_many_short_chunks_default_split(hasher, monkeypatch):
-    """8192 x 1 MiB streams at min 2,000 / max 80,000: 8 GiB is throughput-bound (>= 80,000 << 16
-    bytes), so the default split sends chunks of up to 64 KiB to lanes and the rest to quads;
-    every chunk of a sample of streams = hashlib."""
+@pytest.mark.parametrize('n', [8192, 16384])
+def test_many_short_chunks_default_split(hasher, monkeypatch, n):
+    """n x 1 MiB streams at min 2,000 / max 80,000, throughput-bound (>= 80,000 << 16 bytes): at
+    8 GiB the default split sends chunks of up to 64 KiB to lanes and the rest to quads (the
+    fused kernel); at 16 GiB every chunk fits a lane (up to 128 KiB: the lane kernel).  Every
+    chunk of a sample of streams = hashlib."""
     monkeypatch.delenv('RC_B2_LANE_MAX', raising=False)
-    n, size = 8192, 1 << 20
+    monkeypatch.delenv('RC_B2_LANE_ONLY', raising=False)
+    size = 1 << 20
     ch = GpuChunker(2_000, 80_000, b'\xff' * 16)
     ts, res = D._chunk_and_digest(ch, hasher, [size] * n)
     short = 0
-    for i in list(range(0, n, 193)) + [n - 1]:
+    for i in list(range(0, n, n // 40 + 1)) + [n - 1]:
         data = synth.stream_bytes(size, synth.DEFAULT_SEED, i).tobytes()
         ends, dig = res[i]
         prev = 0
