@@ -75,6 +75,14 @@ def parse(argv=None):
                    help='CPU-baseline processes (default: the cores this process may use)')
     p.add_argument('--e2e', action='store_true', help='also time the host-resident path')
     p.add_argument('--no-verify', action='store_true')
+    p.add_argument('--pipeline', choices=['on', 'off'], default='on',
+                   help='on: steps are RC_PIPELINED calls -- the tile kernel on all but '
+                        '--reserve-cus CUs, edge + chain kernels on those, so one step\'s chain '
+                        'runs beside the next step\'s tile kernel; off: every kernel of a step '
+                        'on one stream, in sequence')
+    p.add_argument('--reserve-cus', type=int, default=0,
+                   help='CUs kept for the chain kernels in pipelined steps (0: the library '
+                        'default)')
     p.add_argument('--share-gpus', action='store_true',
                    help='allow ranks to share a device (a rehearsal of the N-rank path on a '
                         'smaller box; the line then carries no roofline)')
@@ -140,6 +148,9 @@ class Backend:
         # main() refuses that (distinct physical devices checked) unless --share-gpus
         self.index = local_rank % max(1, torch.cuda.device_count())
         torch.cuda.set_device(self.index)
+        # every bench op on one non-blocking stream: the legacy NULL stream would synchronise
+        # with the chunker's CU-masked streams (blocking streams) and serialise pipelined steps
+        torch.cuda.set_stream(torch.cuda.Stream())
 
     def identity(self):
         """The physical device this rank runs on: ordinal, PCI location, UUID, name."""
@@ -514,9 +525,10 @@ class Config3ii:
     speculative chain, the ranks exchange their cut lists through a host-side (gloo) gather and
     splice them.  One rank: the plain single-stream path (segment-parallel chain on one GPU)."""
 
-    def __init__(self, ch, size, ranks, be):
+    def __init__(self, ch, size, ranks, be, pipelined=False):
         from replicat_amd import split, synth
         self.ch, self.ranks, self.be = ch, ranks, be
+        self.pipelined = pipelined
         self.rank, self.world = ranks.rank, ranks.world
         self.hs = be.stream()
         self.L = size * self.world
@@ -534,9 +546,9 @@ class Config3ii:
         self.ends = None
         self.rounds = 0
 
-    def enqueue(self, w, entry):
+    def enqueue(self, w, entry, pipelined=False):
         """Chunk window w from ``entry`` on the device (cut ends relative to entry in
-        self.cuts / the returned tensor); enqueue only."""
+        self.cuts / the returned tensor); enqueue only (pipelined: ch.wait orders the outputs)."""
         off = entry - w.start
         src, n = self.buf.data_ptr() + off, w.end - entry
         tmp = None
@@ -547,7 +559,8 @@ class Config3ii:
         _, caps = self.ch.capacity([n])
         cuts = self.cuts if int(caps[0]) <= self.cap else self.be.zeros_i64(int(caps[0]))
         self.ch.chunk_device([src], [n], [max(0, w.last_piece - off) if not w.open else 0],
-                             cuts.data_ptr(), self.counts.data_ptr(), self.hs, open_=w.open)
+                             cuts.data_ptr(), self.counts.data_ptr(), self.hs, open_=w.open,
+                             pipelined=pipelined)
         self._tmp = tmp
         return cuts
 
@@ -566,7 +579,9 @@ class Config3ii:
         window's speculative one -- the whole lists only when that fails (split.chunk_split)."""
         from replicat_amd import split
         self.ends, self._bounds = None, None
-        cuts = self.enqueue(self.w, self.w.start)
+        # one rank: steps pipeline (nothing is read back between them); several: each step
+        # reads its window's head and tail back, so its calls run in sequence
+        cuts = self.enqueue(self.w, self.w.start, pipelined=self.pipelined and self.world == 1)
         self._cuts = cuts
         if self.world == 1:
             return
@@ -712,10 +727,12 @@ def main(argv=None, backend=Backend):
     custom = (min_len, max_len) != (cfg[2], cfg[3])
     ch = be.chunker(min_len, max_len, key)
     hs = be.stream()
+    pipelined = args.pipeline == 'on'
+    reserve = ch.overlap(args.reserve_cus) if pipelined else 0
     last = None
     edit = long = harness = None
     if args.config == '3ii':
-        long = Config3ii(ch, size, ranks, be)
+        long = Config3ii(ch, size, ranks, be, pipelined)
         n, lens = 1, long.lens
         base_ptr = long.buf.data_ptr()
         last = [long.w.last_piece if not long.w.open else 0]
@@ -757,25 +774,33 @@ def main(argv=None, backend=Backend):
         lens_a = np.ascontiguousarray(lens, dtype=np.uint64)
         last_a = np.ascontiguousarray(last if last is not None else np.zeros(n), dtype=np.uint64)
 
-    def step():
+    def step(pipe=pipelined):
         if long is not None:
-            long.step()
+            if pipe == pipelined:
+                long.step()
+            else:
+                long.enqueue(long.w, long.w.start, pipelined=pipe)
         else:
-            ch.chunk_device(ptrs_a, lens_a, last_a, cuts.data_ptr(), counts.data_ptr(), hs)
+            ch.chunk_device(ptrs_a, lens_a, last_a, cuts.data_ptr(), counts.data_ptr(), hs,
+                            pipelined=pipe)
 
     for _ in range(args.warmup):
         step()
+    ch.wait(hs)
     be.synchronize()
     ranks.barrier()
     be.synchronize()
     ch.timing(True)
+    piped0 = ch.pipelined_calls()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    ch.wait(hs)  # the outputs of every step (pipelined steps leave hs free)
     be.synchronize()
     ranks.barrier()
     be.synchronize()
     elapsed = time.perf_counter() - t0
+    piped = ch.pipelined_calls() - piped0
     ch.timing(False)
     tile_ms, edge_ms, chain_ms, calls = ch.read_kernel_timing()
     mine = {'rank': rank, 'elapsed_s': round(elapsed, 6),
@@ -798,6 +823,18 @@ def main(argv=None, backend=Backend):
         if not custom:
             parity, scope = check_parity(args, n, size, rank, long, edit, ends, digest)
     LAST.update(device=be.index, ends=ends, parity=parity, rank=rank)
+    # the same step unpipelined (every kernel on one stream in sequence), after the timed
+    # region: what one call takes from its first kernel to its cuts
+    seq_ms = None
+    if pipelined and (long is None or world == 1):
+        seq = max(1, min(3, args.steps))
+        step(False)
+        be.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(seq):
+            step(False)
+        be.synchronize()
+        seq_ms = (time.perf_counter() - t1) * 1e3 / seq
     mine['parity'] = parity
     per_rank = ranks.gather(mine)
     flags = [r['parity'] for r in per_rank]
@@ -850,6 +887,13 @@ def main(argv=None, backend=Backend):
             'steps': args.steps,
             'warmup': args.warmup,
             'ms_per_step': round(ms_per_step, 3),
+            'pipeline': {'on': pipelined, 'reserve_cus': reserve, 'pipelined_steps': piped,
+                         'unpipelined_ms_per_step': None if seq_ms is None else round(seq_ms, 3),
+                         'note': 'steps are RC_PIPELINED calls: step k\'s edge + chain kernels '
+                                 'run on the reserved CUs beside step k+1\'s tile kernel (the '
+                                 'library runs small-window and static-schedule batches in '
+                                 'sequence: pipelined_steps counts the overlapped ones); every '
+                                 'step still computes every cut'} if pipelined else {'on': False},
             'higher_is_better': True,
             'scaling': 'weak',
             'vs_baseline': None,

@@ -44,6 +44,20 @@ extern "C" {
                       rule (the adapter's non-final next_cut calls, adapters.py:295-301); the
                       uncut remainder starts at the last reported cut (0 if none).  last_piece is
                       ignored. */
+#define RC_PIPELINED 2u /* (rc_chunk_device) run the call on the chunker's two CU-partitioned
+                      streams (rc_chunker_overlap): the tile kernel on most CUs, the edge and
+                      chain kernels on the reserved ones, so that this call's chain runs beside
+                      the NEXT call's tile kernel.  The tile kernel waits for the work queued on
+                      hip_stream before the call (the inputs); hip_stream does not wait for the
+                      outputs -- rc_chunk_wait does.  Same cuts as without the flag.  The
+                      chunker's streams are blocking streams (HIP creates CU-masked streams so):
+                      a caller on the legacy NULL stream gets correct but serial calls, so
+                      pipelined callers use a non-blocking stream.  Calls the overlap does not
+                      pay for run in sequence on hip_stream instead (a legal schedule of the
+                      flag): chunkers with small windows (max_length below ~1 MB: the chain
+                      does not fit beside the tile kernel) and batches below ~128 tiles of
+                      16 KiB per tile-kernel wave (~8 GiB; the tile kernel's static schedule).
+                      RC_PIPE_ALL=1 in the environment pipelines every call. */
 
 typedef struct rc_chunker rc_chunker;
 
@@ -88,10 +102,27 @@ uint64_t rc_cut_capacity(const rc_chunker *ch, uint64_t n, const uint64_t *lens,
  * d_cuts[cut_base[i] ..] where cut_base = exclusive prefix sum of the capacities of
  * rc_cut_capacity, and the count to d_counts[i] (int64; -1 = capacity overflow).
  * The host arrays are read before return; the work is enqueued on `hip_stream` (a
- * hipStream_t, NULL = default stream) and the call returns without synchronising. */
+ * hipStream_t, NULL = default stream) and the call returns without synchronising.  With
+ * RC_PIPELINED the kernels go to the chunker's own streams instead (see the flag). */
 int rc_chunk_device(rc_chunker *ch, uint64_t n, const uint8_t *const *d_streams,
                     const uint64_t *lens, const uint64_t *last_piece, uint32_t flags,
                     uint64_t *d_cuts, int64_t *d_counts, void *hip_stream);
+
+/* Overlap mode of RC_PIPELINED calls: keep `reserve_cus` CUs (0 = the default, 32, or
+ * RC_OVERLAP_CUS) for the edge and chain kernels and give the tile kernel the rest.  The split
+ * is a pair of CU-masked HIP streams (hipExtStreamCreateWithCUMask; a multiple of 32 reserves
+ * the same number of CUs on every shader engine of every XCD -- anything else leaves engines
+ * unequal, and the persistent tile kernel slows by ~15 %); changing it waits for the pipelined
+ * calls in flight.
+ * rc_chunker_overlap_cus returns the current split (0 before the first pipelined call). */
+int rc_chunker_overlap(rc_chunker *ch, uint32_t reserve_cus);
+uint32_t rc_chunker_overlap_cus(const rc_chunker *ch);
+/* How many RC_PIPELINED calls so far ran on the two streams (the rest ran in sequence). */
+uint64_t rc_chunker_pipelined_calls(const rc_chunker *ch);
+
+/* Make hip_stream wait (device side, no host synchronisation) until every rc_chunk_device call
+ * made so far -- pipelined or not -- has written its cuts and counts. */
+int rc_chunk_wait(rc_chunker *ch, void *hip_stream);
 
 /* The same over HOST-resident streams, blocking: pinned double-buffered H2D copies overlap
  * the kernels of the previous batch; cuts come back to host arrays laid out as above

@@ -27,6 +27,7 @@ RC_ERR_HIP = 12
 RC_ERR_OVERFLOW = 13
 RC_ERR_NO_DEVICE = 14
 RC_OPEN = 1
+RC_PIPELINED = 2
 RC_DIGEST_SLOT = 64
 
 # every symbol include/replicat_chunker.h, replicat_digest.h and replicat_cipher.h declare:
@@ -44,6 +45,10 @@ SIGNATURES = {
     'rc_cut_capacity': (_u64, [_p, _u64, _p, _p]),
     'rc_chunk_device': (_int, [_p, _u64, _p, _p, _p, _u32, _p, _p, _p]),
     'rc_chunk_host': (_int, [_p, _u64, _p, _p, _p, _u32, _p, _p]),
+    'rc_chunker_overlap': (_int, [_p, _u32]),
+    'rc_chunker_overlap_cus': (_u32, [_p]),
+    'rc_chunker_pipelined_calls': (_u64, [_p]),
+    'rc_chunk_wait': (_int, [_p, _p]),
     'rc_timing_enable': (_int, [_p, _int]),
     'rc_timing_read': (_int, [_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                               ctypes.POINTER(_u64)]),

@@ -15,7 +15,7 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from ._lib import RC_OPEN, check, lib
+from ._lib import RC_OPEN, RC_PIPELINED, check, lib
 
 MIN_LENGTH = 128_000     # replicat/utils/adapters.py:259
 MAX_LENGTH = 5_120_000   # replicat/utils/adapters.py:260
@@ -78,15 +78,34 @@ class GpuChunker:
         total = lib().rc_cut_capacity(self._h, len(lens), lens.ctypes.data, caps.ctypes.data)
         return int(total), caps
 
-    def chunk_device(self, ptrs, lens, last_piece, cuts_ptr, counts_ptr, stream=0, open_=False):
+    def chunk_device(self, ptrs, lens, last_piece, cuts_ptr, counts_ptr, stream=0, open_=False,
+                     pipelined=False):
         """Enqueue the chunking of device-resident streams (raw device pointers) on a HIP
         stream; cut END offsets land in the device array at ``cuts_ptr`` (u64, per-stream
-        regions of ``capacity(lens)`` entries) and counts at ``counts_ptr`` (int64)."""
+        regions of ``capacity(lens)`` entries) and counts at ``counts_ptr`` (int64).
+
+        ``pipelined=True`` (RC_PIPELINED): the kernels run on the chunker's CU-partitioned
+        streams, this call's chain beside the next call's tile kernel; ``stream`` orders the
+        inputs only, and ``wait(stream)`` orders the outputs."""
         ptrs, lens = _ptr_array(ptrs), _ptr_array(lens)
         last = _ptr_array(last_piece if last_piece is not None else np.zeros(len(lens)))
+        flags = (RC_OPEN if open_ else 0) | (RC_PIPELINED if pipelined else 0)
         check(lib().rc_chunk_device(self._h, len(lens), ptrs.ctypes.data, lens.ctypes.data,
-                                    last.ctypes.data, RC_OPEN if open_ else 0, cuts_ptr,
-                                    counts_ptr, stream or None))
+                                    last.ctypes.data, flags, cuts_ptr, counts_ptr, stream or None))
+
+    def overlap(self, reserve_cus=0):
+        """CUs kept for the chain kernels of pipelined calls (0 = the default); returns the
+        split in force."""
+        check(lib().rc_chunker_overlap(self._h, int(reserve_cus)))
+        return int(lib().rc_chunker_overlap_cus(self._h))
+
+    def pipelined_calls(self):
+        """Pipelined requests so far that ran on the two streams (the others in sequence)."""
+        return int(lib().rc_chunker_pipelined_calls(self._h))
+
+    def wait(self, stream=0):
+        """Make a HIP stream wait for every call so far (pipelined or not)."""
+        check(lib().rc_chunk_wait(self._h, stream or None))
 
     def chunk_host(self, buffers, last_piece=None, open_=False):
         """Chunk host streams (uint8 arrays / bytes-like); returns a list of cut-END arrays."""

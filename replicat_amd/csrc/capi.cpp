@@ -175,6 +175,7 @@ struct rc_chunker {
         DevBuf d_records;   // one TileRecord per tile
         DevBuf d_scratch;   // speculative chain lists of multi-segment streams
         DevBuf d_seg_counts;  // one count (+ termination bit) per chain segment
+        DevBuf d_ctr;         // the tile kernel's grab counter (zeroed once, then by the edge kernel)
         std::vector<uint64_t> xtiles;  // host list of the tiles the fast path does not take
         hipEvent_t done = nullptr;  // the call that last used this workspace has finished
         bool pending = false;
@@ -193,6 +194,15 @@ struct rc_chunker {
     // previous call's kernels (the workspace alternation keeps the two apart)
     hipStream_t cstream = nullptr;
     hipEvent_t uploaded[2] = {nullptr, nullptr};
+
+    // RC_PIPELINED calls (overlap mode): the tile kernel on `tstream`, whose CU mask leaves out
+    // `reserve` CUs, the edge and chain kernels on `xstream`, masked to exactly those CUs, so
+    // that one call's chain runs beside the next call's tile kernel
+    uint32_t reserve_req = 0;  // rc_chunker_overlap / RC_OVERLAP_CUS (0: kDefaultReserve)
+    uint32_t reserve = 0, tile_cus = 0;  // of the streams below (0: not created)
+    hipStream_t tstream = nullptr, xstream = nullptr;
+    hipEvent_t in_ev[2] = {nullptr, nullptr}, tiled[2] = {nullptr, nullptr};
+    uint64_t pipelined_calls = 0;  // RC_PIPELINED requests that ran on the two streams
 
     // timing: events before the tile kernel, after it, after the edge kernel, after the chain
     bool timing = false;
@@ -280,7 +290,7 @@ Workspace &acquire_ws(rc_chunker *ch) {
 
 int stage_descriptors(rc_chunker *ch, Workspace &ws, uint64_t n, const uint8_t *const *ptrs,
                       const uint64_t *lens, const uint64_t *last, Plan &plan, bool open = false,
-                      bool single = false) {
+                      bool single = false, uint64_t walkers = 0) {
     plan.n = n;
     if (ws.pending) {  // the call that used this workspace before must be done with it
         HIP_TRY(hipEventSynchronize(ws.done));
@@ -314,8 +324,10 @@ int stage_descriptors(rc_chunker *ch, Workspace &ws, uint64_t n, const uint8_t *
     // walkers (4 waves per SIMD): a walker is latency-bound, so shorter chains on more waves
     // finish sooner even with the extension steps and the join (round 2, same box: config 2
     // 0.19 -> 0.15 ms, 3 (ii) 0.31 -> 0.20, config 4 0.47 -> 0.24; 1024 walkers before).
+    // Pipelined calls walk on the reserved CUs only (16 walkers per CU, as 4096 on 256): there
+    // the chain must fit beside the next tile kernel, and fewer segments are less work.
     {
-        constexpr uint64_t kChainWalkers = 4096;
+        const uint64_t kChainWalkers = walkers ? walkers : 4096;
         uint64_t total = 0;
         for (uint64_t i = 0; i < n; ++i) {
             uint64_t b = 0;
@@ -387,18 +399,28 @@ size_t records_bytes(const Plan &plan) {
            rc_tie_list_words(plan.n_tiles) * 4;
 }
 
+// the grab counter: allocated and zeroed once per workspace; every edge kernel leaves it 0
+int ensure_ctr(Workspace &ws) {
+    if (ws.d_ctr.p) return 0;
+    if (int rc = ws.d_ctr.ensure(256)) return rc;
+    HIP_TRY(hipMemset(ws.d_ctr.p, 0, 256));
+    return 0;
+}
+
 // batches of at least this many streams walk their chains one lane per stream (when the
 // windows are small and every stream is one segment: kernels.hip rc_lane_chain_kernel)
 constexpr uint64_t kLaneMinStreams = 256;
 
 int upload_and_launch(rc_chunker *ch, Workspace &ws, const Plan &plan, ChainParams prm,
-                      uint64_t *d_cuts, int64_t *d_counts, hipStream_t stream) {
+                      uint64_t *d_cuts, int64_t *d_counts, hipStream_t stream,
+                      bool pipelined = false) {
     if (int rc = ws.d_desc.ensure(plan.bytes)) return rc;
     // records, then (small windows) the group maxima of every tile, then the tie lists
     if (int rc = ws.d_records.ensure(records_bytes(plan))) return rc;
     if (int rc = ws.d_scratch.ensure(std::max<uint64_t>(plan.scratch_entries, 1) * 8)) return rc;
     // counts, merge points, slice offsets and slices of the parallel join (kernels.hip)
     if (int rc = ws.d_seg_counts.ensure(std::max<uint64_t>(plan.n_segs, 1) * 32)) return rc;
+    if (int rc = ensure_ctr(ws)) return rc;
     // The upload goes on the copy stream: stage_descriptors already waited for the call that
     // last used this workspace, so its device buffer is free now, while the previous call's
     // kernels may still be running on `stream`.  `stream` waits for the upload only.
@@ -407,7 +429,17 @@ int upload_and_launch(rc_chunker *ch, Workspace &ws, const Plan &plan, ChainPara
     if (!ch->uploaded[wi]) HIP_TRY(hipEventCreateWithFlags(&ch->uploaded[wi], hipEventDisableTiming));
     HIP_TRY(hipMemcpyAsync(ws.d_desc.p, ws.h_desc.p, plan.bytes, hipMemcpyHostToDevice, ch->cstream));
     HIP_TRY(hipEventRecord(ch->uploaded[wi], ch->cstream));
-    HIP_TRY(hipStreamWaitEvent(stream, ch->uploaded[wi], 0));
+    // ts: the tile kernel's stream, xs: the edge and chain kernels'.  A pipelined call's tile
+    // kernel waits for what the caller queued on `stream` before the call (its inputs); the
+    // caller's stream waits for nothing (rc_chunk_wait)
+    hipStream_t ts = stream, xs = stream;
+    if (pipelined) {
+        ts = ch->tstream;
+        xs = ch->xstream;
+        HIP_TRY(hipEventRecord(ch->in_ev[wi], stream));
+        HIP_TRY(hipStreamWaitEvent(ts, ch->in_ev[wi], 0));
+    }
+    HIP_TRY(hipStreamWaitEvent(ts, ch->uploaded[wi], 0));
     const StreamDesc d = desc_view(ws.d_desc.p, plan.n);
     std::array<hipEvent_t, 4> ev{};
     if (ch->timing) {
@@ -419,7 +451,7 @@ int upload_and_launch(rc_chunker *ch, Workspace &ws, const Plan &plan, ChainPara
                 ch->ev_pool.pop_back();
             }
         }
-        HIP_TRY(hipEventRecord(ev[0], stream));
+        HIP_TRY(hipEventRecord(ev[0], ts));
     }
     GroupRecord *grp = ch->groups ? group_records(ws, plan) : nullptr;
     prm.grp = grp;
@@ -439,20 +471,66 @@ int upload_and_launch(rc_chunker *ch, Workspace &ws, const Plan &plan, ChainPara
     prm.hot = group_hot_threshold(ch->window);
     if (rc_launch_tiles(ch->d_tables, d, plan.n, plan.n_tiles,
                         static_cast<TileRecord *>(ws.d_records.p), grp, prm.hot, tie_lists(ws, plan),
-                        stream, ch->timing ? ev[1] : nullptr))
+                        static_cast<uint32_t *>(ws.d_ctr.p), ts, ch->timing ? ev[1] : nullptr,
+                        pipelined ? ch->tile_cus : 0u,
+                        xs, pipelined ? ch->tiled[wi] : nullptr))
         return fail(RC_ERR_HIP, "%s", rc_launch_error());
-    if (ch->timing) HIP_TRY(hipEventRecord(ev[2], stream));
+    if (ch->timing) HIP_TRY(hipEventRecord(ev[2], xs));
     if (rc_launch_chain(ch->d_tables, d, plan.n, prm, plan.n_segs,
                         static_cast<const TileRecord *>(ws.d_records.p), d_cuts, d_counts,
                         static_cast<uint64_t *>(ws.d_scratch.p),
-                        static_cast<uint64_t *>(ws.d_seg_counts.p), plan.any_multi, stream))
+                        static_cast<uint64_t *>(ws.d_seg_counts.p), plan.any_multi, xs))
         return fail(RC_ERR_HIP, "%s", rc_launch_error());
-    HIP_TRY(hipEventRecord(ws.done, stream));
+    HIP_TRY(hipEventRecord(ws.done, xs));
     ws.pending = true;
     if (ch->timing) {
-        HIP_TRY(hipEventRecord(ev[3], stream));
+        HIP_TRY(hipEventRecord(ev[3], xs));
         ch->ev_rec.push_back(ev);
     }
+    return 0;
+}
+
+// CUs reserved for the edge and chain kernels of pipelined calls when rc_chunker_overlap /
+// RC_OVERLAP_CUS do not say: one per shader engine (4 per XCD).  Measured on one allocation
+// (scripts/overlap_ab.py, profiles/r03/overlap/): reserving 8 or 16 CUs left the shader
+// engines of an XCD unequal and the persistent tile kernel 15 % slower (config 2: 11.3 and
+// 11.7 ms against 9.87 unpipelined -- a workgroup the dispatcher sends to a full engine waits
+// for the end of the launch); 32 keeps every engine at 7 CUs and the tile kernel at 9.84 ms.
+constexpr uint32_t kDefaultReserve = 32;
+
+// The two streams of overlap mode.  KFD spreads the bits of a queue's CU mask over the XCDs
+// first (bit i -> XCD i % 8), then over that XCD's shader engines (bits 0-7 engine 0, 8-15
+// engine 1, ...), so the first `reserve` bits take reserve / 8 CUs of every XCD and, for a
+// multiple of 32, the same number of every engine (scripts/ubench/cumask_probe.hip reads the
+// CUs each mask runs on: disjoint, 2 or 4 per XCD).
+int setup_overlap(rc_chunker *ch) {
+    uint32_t want = ch->reserve_req;
+    if (!want) {
+        want = kDefaultReserve;
+        if (const char *e = getenv("RC_OVERLAP_CUS")) want = (uint32_t)strtoul(e, nullptr, 0);
+    }
+    if (ch->tstream && ch->reserve == want) return 0;
+    int cus = 0;
+    HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ch->device));
+    if (want == 0 || (int)want >= cus)
+        return fail(RC_ERR_ARGUMENT, "overlap: %u reserved CUs of %d", want, cus);
+    if (ch->tstream) {  // a different split: retire the old pair
+        HIP_TRY(hipStreamSynchronize(ch->tstream));
+        HIP_TRY(hipStreamSynchronize(ch->xstream));
+        (void)hipStreamDestroy(ch->tstream);
+        (void)hipStreamDestroy(ch->xstream);
+        ch->tstream = ch->xstream = nullptr;
+    }
+    std::vector<uint32_t> tm((cus + 31) / 32, 0u), xm((cus + 31) / 32, 0u);
+    for (int i = 0; i < cus; ++i) ((uint32_t)i < want ? xm : tm)[i / 32] |= 1u << (i % 32);
+    HIP_TRY(hipExtStreamCreateWithCUMask(&ch->tstream, (uint32_t)tm.size(), tm.data()));
+    HIP_TRY(hipExtStreamCreateWithCUMask(&ch->xstream, (uint32_t)xm.size(), xm.data()));
+    for (int i = 0; i < 2; ++i) {
+        if (!ch->in_ev[i]) HIP_TRY(hipEventCreateWithFlags(&ch->in_ev[i], hipEventDisableTiming));
+        if (!ch->tiled[i]) HIP_TRY(hipEventCreateWithFlags(&ch->tiled[i], hipEventDisableTiming));
+    }
+    ch->reserve = want;
+    ch->tile_cus = (uint32_t)cus - want;
     return 0;
 }
 
@@ -588,6 +666,7 @@ void rc_chunker_destroy(rc_chunker *ch) {
             w.d_records.release();
             w.d_scratch.release();
             w.d_seg_counts.release();
+            w.d_ctr.release();
             w.h_desc.release();
             if (w.done) (void)hipEventDestroy(w.done);
         }
@@ -602,8 +681,14 @@ void rc_chunker_destroy(rc_chunker *ch) {
         }
         ch->h_out.release();
         if (ch->cstream) (void)hipStreamDestroy(ch->cstream);
+        if (ch->tstream) (void)hipStreamDestroy(ch->tstream);
+        if (ch->xstream) (void)hipStreamDestroy(ch->xstream);
         for (auto e : ch->uploaded)
             if (e) (void)hipEventDestroy(e);
+        for (int i = 0; i < 2; ++i) {
+            if (ch->in_ev[i]) (void)hipEventDestroy(ch->in_ev[i]);
+            if (ch->tiled[i]) (void)hipEventDestroy(ch->tiled[i]);
+        }
         for (auto &r : ch->ev_rec)
             for (auto e : r) (void)hipEventDestroy(e);
         for (auto e : ch->ev_pool) (void)hipEventDestroy(e);
@@ -706,14 +791,62 @@ int rc_chunk_device(rc_chunker *ch, uint64_t n, const uint8_t *const *d_streams,
     if (n == 0) return RC_OK;
     if (!d_cuts || !d_counts) return fail(RC_ERR_ARGUMENT, "null output arrays");
     const bool open = (flags & RC_OPEN) != 0;
+    // Two kinds of call run a pipelined request in sequence on the caller's stream -- a legal
+    // schedule of the flag (inputs and outputs in that stream's order) -- because the overlap
+    // cost more than it hid (scripts/overlap_ab.py, profiles/r03/overlap/):
+    // * small windows (group records, lane / quad chains: config 3 iii): their chain takes
+    //   2.8 ms on 32 CUs and their VALU-heavier tile kernel lost 3 % on 224 CUs;
+    // * launches on the tile kernel's static schedule (fewer than 128 tiles per wave: the
+    //   harness's one 5.12 GB stream): on 224 CUs the static shares grow, 0.85 -> 0.92 ms.
+    // RC_PIPE_ALL=1 pipelines every call (tests, measurements).
+    const char *pa = getenv("RC_PIPE_ALL");
+    const bool all = pa && pa[0] == '1';
+    bool pipelined = (flags & RC_PIPELINED) != 0 && (all || !ch->groups);
+    if (pipelined && !all) {
+        uint64_t tiles = 0;
+        for (uint64_t i = 0; i < n; ++i) {
+            const uint64_t P = open ? lens[i] : last_piece ? last_piece[i] : 0;
+            const uint64_t jn = rc_keys_needed(ch->max_length, lens[i], P);
+            tiles += jn ? jn / kTileKeys + 1 : 0;
+        }
+        pipelined = rc_tile_dynamic(tiles, 0) != 0;
+    }
+    ch->pipelined_calls += pipelined ? 1 : 0;
     if (int rc = validate_streams(n, d_streams, lens, open ? nullptr : last_piece, true)) return rc;
     std::lock_guard<std::mutex> lock(ch->mu);
     DeviceGuard g(ch->device);
+    if (pipelined)
+        if (int rc = setup_overlap(ch)) return rc;
     Plan plan;
     Workspace &ws = acquire_ws(ch);
-    if (int rc = stage_descriptors(ch, ws, n, d_streams, lens, last_piece, plan, open)) return rc;
+    if (int rc = stage_descriptors(ch, ws, n, d_streams, lens, last_piece, plan, open, false,
+                                   pipelined ? 16ull * ch->reserve : 0))
+        return rc;
     return upload_and_launch(ch, ws, plan, chain_params(ch, plan, ~0ull, flags), d_cuts, d_counts,
-                             static_cast<hipStream_t>(hip_stream));
+                             static_cast<hipStream_t>(hip_stream), pipelined);
+}
+
+int rc_chunker_overlap(rc_chunker *ch, uint32_t reserve_cus) {
+    if (!ch) return fail(RC_ERR_ARGUMENT, "null chunker");
+    std::lock_guard<std::mutex> lock(ch->mu);
+    DeviceGuard g(ch->device);
+    ch->reserve_req = reserve_cus;
+    return setup_overlap(ch);
+}
+
+uint32_t rc_chunker_overlap_cus(const rc_chunker *ch) { return ch ? ch->reserve : 0u; }
+
+uint64_t rc_chunker_pipelined_calls(const rc_chunker *ch) { return ch ? ch->pipelined_calls : 0; }
+
+int rc_chunk_wait(rc_chunker *ch, void *hip_stream) {
+    if (!ch) return fail(RC_ERR_ARGUMENT, "null chunker");
+    std::lock_guard<std::mutex> lock(ch->mu);
+    DeviceGuard g(ch->device);
+    // a workspace's `done` was recorded by its last call, after the host had waited for the
+    // call before that one on the same workspace: the two events cover every call so far
+    for (auto &w : ch->ws)
+        HIP_TRY(hipStreamWaitEvent(static_cast<hipStream_t>(hip_stream), w.done, 0));
+    return RC_OK;
 }
 
 }  // extern "C"
@@ -851,12 +984,13 @@ int rc_tile_records(rc_chunker *ch, uint64_t n, const uint8_t *const *d_streams,
     if (int rc = stage_descriptors(ch, ws, n, d_streams, lens, last_piece, plan)) return rc;
     if (int rc = ws.d_desc.ensure(plan.bytes)) return rc;
     if (int rc = ws.d_records.ensure(records_bytes(plan))) return rc;
+    if (int rc = ensure_ctr(ws)) return rc;
     HIP_TRY(hipMemcpy(ws.d_desc.p, ws.h_desc.p, plan.bytes, hipMemcpyHostToDevice));
     GroupRecord *d_grp = ch->groups ? group_records(ws, plan) : nullptr;
     if (rc_launch_tiles(ch->d_tables, desc_view(ws.d_desc.p, n), n, plan.n_tiles,
                         static_cast<TileRecord *>(ws.d_records.p), d_grp,
                         group_hot_threshold(ch->window), tie_lists(ws, plan),
-                        nullptr, nullptr))
+                        static_cast<uint32_t *>(ws.d_ctr.p), nullptr, nullptr, 0u, nullptr, nullptr))
         return fail(RC_ERR_HIP, "%s", rc_launch_error());
     HIP_TRY(hipDeviceSynchronize());
     std::vector<TileRecord> h(plan.n_tiles);

@@ -127,11 +127,19 @@ extern "C" {
 // the chain's bounds for small windows.  mid_event (a hipEvent_t, may be NULL):
 // recorded between the tile and the edge kernel.
 // d_xlist: rc_tie_list_words(n_tiles) u32 of scratch: the tile kernel's tie lists (n_tiles
-// slots), one count per work unit and the dynamic units' grab counter (zeroed per launch).
+// slots) and one count per work unit.  d_ctr: the dynamic units' grab counter, 0 at the call;
+// the edge kernel zeros it again for the next launch.
+// cus: the CUs the tile kernel's stream may use (its persistent grid; 0 = every CU of the
+// device).  edge_stream (may be NULL = stream): where the edge kernel runs; when it differs,
+// `tiled` (a hipEvent_t) is recorded after the tile kernel and edge_stream waits for it.
 int rc_launch_tiles(const rc::KeyTables *d_tables, rc::StreamDesc desc, uint64_t n_streams,
                     uint64_t n_tiles, rc::TileRecord *d_records, rc::GroupRecord *d_grp,
-                    uint32_t hot, uint32_t *d_xlist, void *stream, void *mid_event);
+                    uint32_t hot, uint32_t *d_xlist, uint32_t *d_ctr, void *stream,
+                    void *mid_event, uint32_t cus, void *edge_stream, void *tiled);
 uint64_t rc_tie_list_words(uint64_t n_tiles);
+// 1 if a tile launch over n_tiles on `cus` CUs (0 = all) hands out dynamic units, 0 if it is
+// fully static (fewer than kDynMinPerWave tiles per wave)
+int rc_tile_dynamic(uint64_t n_tiles, uint32_t cus);
 int rc_launch_chain(const rc::KeyTables *d_tables, rc::StreamDesc desc, uint64_t n_streams,
                     rc::ChainParams prm, uint64_t n_segs, const rc::TileRecord *d_records,
                     uint64_t *d_cuts, int64_t *d_counts, uint64_t *d_scratch,

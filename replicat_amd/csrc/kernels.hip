@@ -856,8 +856,12 @@ __global__ __launch_bounds__(256) void rc_edge_kernel(const KeyTables *__restric
                                                       TileRecord *__restrict__ rec,
                                                       GroupRecord *__restrict__ grp,
                                                       const uint32_t *__restrict__ xlist,
-                                                      const uint32_t *__restrict__ xcount) {
+                                                      const uint32_t *__restrict__ xcount,
+                                                      uint32_t *__restrict__ ctr) {
     __shared__ __attribute__((aligned(16))) uint64_t s_full[2048];
+    // the tile kernel is done with its grab counter: zero it for the workspace's next launch
+    // (round 3: replaces a hipMemsetAsync between consecutive tile kernels)
+    if (blockIdx.x == 0 && threadIdx.x == 0) *ctr = 0u;
     const uint64_t gw = (uint64_t)blockIdx.x * (blockDim.x >> 6) +
                         __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
@@ -2771,25 +2775,32 @@ int rc_diag_read(uint64_t *out, uint32_t cap, uint32_t *n) {
 
 int rc_launch_tiles(const KeyTables *d_tables, StreamDesc desc, uint64_t n_streams,
                     uint64_t n_tiles, TileRecord *d_records, GroupRecord *d_grp,
-                    uint32_t hot, uint32_t *d_xlist, void *stream, void *mid_event) {
+                    uint32_t hot, uint32_t *d_xlist, uint32_t *d_ctr, void *stream,
+                    void *mid_event, uint32_t tile_cus, void *edge_stream, void *tiled) {
     hipStream_t st = (hipStream_t)stream;
+    hipStream_t est = edge_stream ? (hipStream_t)edge_stream : st;
+    // the edge kernel's stream follows the tile kernel (also when there are no tiles)
+    auto hand_over = [&]() -> int {
+        if (est == st) return 0;
+        if (hipEventRecord((hipEvent_t)tiled, st) != hipSuccess ||
+            hipStreamWaitEvent(est, (hipEvent_t)tiled, 0) != hipSuccess) {
+            snprintf(g_launch_err, sizeof g_launch_err, "edge stream hand-over failed");
+            return 1;
+        }
+        return 0;
+    };
     if (n_tiles == 0) {
         if (mid_event && hipEventRecord((hipEvent_t)mid_event, st) != hipSuccess) return 1;
-        return 0;
+        return hand_over();
     }
     const uint64_t waves_per_wg = 1024 / kWaveSize;
     uint64_t grid = (n_tiles + waves_per_wg - 1) / waves_per_wg;
-    const uint64_t cus = (uint64_t)cu_count();
+    const uint64_t cus = tile_cus ? (uint64_t)tile_cus : (uint64_t)cu_count();
     if (grid > cus) grid = cus;  // persistent: one 144 KiB-LDS workgroup per CU
     const uint64_t n_waves = grid * waves_per_wg;
     const TileUnits U = tile_units(n_tiles, n_waves);
-    // the tie lists: n_tiles slots, one count per unit, the grab counter
+    // the tie lists: n_tiles slots, one count per unit; d_ctr is 0 (the edge kernel re-zeros it)
     uint32_t *d_xcount = d_xlist + n_tiles;
-    uint32_t *d_ctr = d_xcount + U.n_units;
-    if (U.n_units > U.nw && hipMemsetAsync(d_ctr, 0, sizeof(uint32_t), st) != hipSuccess) {
-        snprintf(g_launch_err, sizeof g_launch_err, "hipMemsetAsync failed");
-        return 1;
-    }
     if (d_grp)
         hipLaunchKernelGGL(rc_tile_kernel<kTileGroups>, dim3((unsigned)grid), dim3(1024), 0, st,
                            d_tables, desc, n_streams, U, d_records, d_grp, hot, d_xlist,
@@ -2802,20 +2813,27 @@ int rc_launch_tiles(const KeyTables *d_tables, StreamDesc desc, uint64_t n_strea
         snprintf(g_launch_err, sizeof g_launch_err, "hipEventRecord failed");
         return 1;
     }
+    if (hand_over()) return 1;
     // one wave per tie list (almost always empty) and per host-listed tile, grid-strided
     uint64_t egrid = (U.n_units + 3) / 4;
     if (egrid > 4 * cus) egrid = 4 * cus;
     if (egrid == 0) egrid = 1;
-    hipLaunchKernelGGL(rc_edge_kernel, dim3((unsigned)egrid), dim3(256), 0, st, d_tables, desc,
+    hipLaunchKernelGGL(rc_edge_kernel, dim3((unsigned)egrid), dim3(256), 0, est, d_tables, desc,
                        n_streams, U, d_records, d_grp, (const uint32_t *)d_xlist,
-                       (const uint32_t *)d_xcount);
+                       (const uint32_t *)d_xcount, d_ctr);
     return launch_status("rc_edge_kernel");
 }
 
 uint64_t rc_tie_list_words(uint64_t n_tiles) {
     // n_tiles list slots + one count per unit (static units: at most n_tiles + 15 waves;
-    // dynamic: at most n_tiles / kDynChunkMin + 1) + the grab counter
+    // dynamic: at most n_tiles / kDynChunkMin + 1)
     return 2 * n_tiles + n_tiles / kDynChunkMin + 64;
+}
+
+int rc_tile_dynamic(uint64_t n_tiles, uint32_t cus) {
+    if (n_tiles == 0) return 0;
+    const TileUnits U = tile_units(n_tiles, (uint64_t)(cus ? cus : (uint32_t)cu_count()) * (1024 / kWaveSize));
+    return U.n_units > U.nw;
 }
 
 int rc_launch_chain(const KeyTables *d_tables, StreamDesc desc, uint64_t n_streams,

@@ -30,13 +30,25 @@ class OracleChunker:
         self.o, self.log = o, log
         self.min_length, self.max_length, self.key = min_length, max_length, key
         self.calls = 0
+        self.pipelined_calls_n = 0
+
+    def overlap(self, reserve_cus=0):
+        return reserve_cus or 32
+
+    def wait(self, stream=0):
+        pass
+
+    def pipelined_calls(self):
+        return self.pipelined_calls_n
 
     def capacity(self, lens):
         step = max(4, (self.min_length + 3) & ~3)
         caps = np.array([int(L) // step + 3 for L in lens], dtype=np.uint64)
         return int(caps.sum()), caps
 
-    def chunk_device(self, ptrs, lens, last, cuts_ptr, counts_ptr, stream=0, open_=False):
+    def chunk_device(self, ptrs, lens, last, cuts_ptr, counts_ptr, stream=0, open_=False,
+                     pipelined=False):
+        self.pipelined_calls_n += bool(pipelined)
         _, caps = self.capacity(lens)
         base = np.concatenate([[0], np.cumsum(caps)[:-1]]).astype(np.int64)
         n = len(lens)

@@ -24,12 +24,15 @@ def device_streams(sizes, seed=None, fill=None, datas=None, ids=None):
     return out
 
 
-def chunk_device(ch: GpuChunker, tensors, sizes, last=None, open_=False):
+def chunk_device(ch: GpuChunker, tensors, sizes, last=None, open_=False, pipelined=False):
     total, caps = ch.capacity(sizes)
     cuts = torch.zeros(max(total, 1), dtype=torch.int64, device='cuda')
     counts = torch.zeros(len(sizes), dtype=torch.int64, device='cuda')
+    hs = torch.cuda.current_stream().cuda_stream
     ch.chunk_device([t.data_ptr() for t in tensors], sizes, last, cuts.data_ptr(),
-                    counts.data_ptr(), torch.cuda.current_stream().cuda_stream, open_)
+                    counts.data_ptr(), hs, open_, pipelined=pipelined)
+    if pipelined:
+        ch.wait(hs)
     torch.cuda.synchronize()
     cuts = cuts.cpu().numpy().view(np.uint64)
     counts = counts.cpu().numpy()
