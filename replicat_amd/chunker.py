@@ -99,6 +99,11 @@ class GpuChunker:
         check(lib().rc_chunker_overlap(self._h, int(reserve_cus)))
         return int(lib().rc_chunker_overlap_cus(self._h))
 
+    def overlap_cus(self):
+        """CUs reserved for pipelined chains (0 until the first pipelined call sets them up,
+        or when the CU-masked streams could not be created)."""
+        return int(lib().rc_chunker_overlap_cus(self._h))
+
     def pipelined_calls(self):
         """Pipelined requests so far that ran on the two streams (the others in sequence)."""
         return int(lib().rc_chunker_pipelined_calls(self._h))

@@ -203,6 +203,7 @@ struct rc_chunker {
     hipStream_t tstream = nullptr, xstream = nullptr;
     hipEvent_t in_ev[2] = {nullptr, nullptr}, tiled[2] = {nullptr, nullptr};
     uint64_t pipelined_calls = 0;  // RC_PIPELINED requests that ran on the two streams
+    bool overlap_failed = false;   // the masked streams could not be created (calls run in sequence)
 
     // timing: events before the tile kernel, after it, after the edge kernel, after the chain
     bool timing = false;
@@ -791,6 +792,7 @@ int rc_chunk_device(rc_chunker *ch, uint64_t n, const uint8_t *const *d_streams,
     if (n == 0) return RC_OK;
     if (!d_cuts || !d_counts) return fail(RC_ERR_ARGUMENT, "null output arrays");
     const bool open = (flags & RC_OPEN) != 0;
+    if (int rc = validate_streams(n, d_streams, lens, open ? nullptr : last_piece, true)) return rc;
     // Two kinds of call run a pipelined request in sequence on the caller's stream -- a legal
     // schedule of the flag (inputs and outputs in that stream's order) -- because the overlap
     // cost more than it hid (scripts/overlap_ab.py, profiles/r03/overlap/):
@@ -811,12 +813,17 @@ int rc_chunk_device(rc_chunker *ch, uint64_t n, const uint8_t *const *d_streams,
         }
         pipelined = rc_tile_dynamic(tiles, 0) != 0;
     }
-    ch->pipelined_calls += pipelined ? 1 : 0;
-    if (int rc = validate_streams(n, d_streams, lens, open ? nullptr : last_piece, true)) return rc;
+
     std::lock_guard<std::mutex> lock(ch->mu);
     DeviceGuard g(ch->device);
-    if (pipelined)
-        if (int rc = setup_overlap(ch)) return rc;
+    // no CU-masked streams on this device / runtime: the request runs in sequence (the call
+    // stays correct; rc_chunker_overlap reports the error, rc_chunker_overlap_cus stays 0)
+    if (pipelined && !ch->overlap_failed && setup_overlap(ch) != 0) {
+        ch->overlap_failed = true;
+        fprintf(stderr, "replicat_amd: pipelined calls run in sequence: %s\n", g_err);
+    }
+    if (ch->overlap_failed && !ch->tstream) pipelined = false;
+    ch->pipelined_calls += pipelined ? 1 : 0;
     Plan plan;
     Workspace &ws = acquire_ws(ch);
     if (int rc = stage_descriptors(ch, ws, n, d_streams, lens, last_piece, plan, open, false,
@@ -831,7 +838,9 @@ int rc_chunker_overlap(rc_chunker *ch, uint32_t reserve_cus) {
     std::lock_guard<std::mutex> lock(ch->mu);
     DeviceGuard g(ch->device);
     ch->reserve_req = reserve_cus;
-    return setup_overlap(ch);
+    const int rc = setup_overlap(ch);
+    ch->overlap_failed = rc != 0 && !ch->tstream;
+    return rc;
 }
 
 uint32_t rc_chunker_overlap_cus(const rc_chunker *ch) { return ch ? ch->reserve : 0u; }

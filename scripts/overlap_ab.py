@@ -95,3 +95,5 @@ for s, v in res.items():
               'tile_ms': round(float(med[1]), 4), 'edge_chain_ms': round(float(med[2]), 4),
               'GiBps': round(float(np.sum(lens)) / (med[0] * 1e-3) / 2**30, 1)}
 print(json.dumps(out), flush=True)
+torch.cuda.synchronize()
+ch.close()  # the CU-masked streams go while the runtime is up

@@ -35,6 +35,9 @@ class OracleChunker:
     def overlap(self, reserve_cus=0):
         return reserve_cus or 32
 
+    def overlap_cus(self):
+        return 32
+
     def wait(self, stream=0):
         pass
 
