@@ -854,6 +854,11 @@ def main(argv=None, backend=Backend):
             else (None, 'seeded key: no PMC summary')
         roof = roofline(bytes_per_step, bytes_needed(max_len, lens, last), tile_ms / calls,
                         edge_ms / calls, chain_ms / calls, traffic, traffic_src, bid)
+        if piped:
+            roof['timing_note'] = (
+                'pipelined steps: kernel_ms is the tile kernel on its CU-masked stream; '
+                'edge_kernel_ms and chain_kernel_ms run on the reserved CUs beside the next '
+                "step's tile kernel and span from the tile kernel's end (waits included)")
         if shared:
             # ranks on one device: each rank's HIP events also time the other ranks' kernels
             roof.update(achieved=None, frac=None, achieved_read=None, frac_read=None,
