@@ -148,9 +148,13 @@ class Backend:
         # main() refuses that (distinct physical devices checked) unless --share-gpus
         self.index = local_rank % max(1, torch.cuda.device_count())
         torch.cuda.set_device(self.index)
-        # every bench op on one non-blocking stream: the legacy NULL stream would synchronise
-        # with the chunker's CU-masked streams (blocking streams) and serialise pipelined steps
-        torch.cuda.set_stream(torch.cuda.Stream())
+
+    def use_own_stream(self):
+        """Make every later bench op run on one non-blocking stream (main() calls this before
+        it allocates anything): the legacy NULL stream would synchronise with the chunker's
+        CU-masked streams (blocking streams) and serialise pipelined steps.  Not done in
+        __init__: tests build a Backend inside their own stream context."""
+        self.torch.cuda.set_stream(self.torch.cuda.Stream())
 
     def identity(self):
         """The physical device this rank runs on: ordinal, PCI location, UUID, name."""
@@ -715,6 +719,8 @@ def main(argv=None, backend=Backend):
     ranks = Ranks()
     world, rank = ranks.world, ranks.rank
     be = backend(ranks.local)
+    if hasattr(be, 'use_own_stream'):
+        be.use_own_stream()
     devices, shared = check_ranks(args, ranks, be)
 
     from replicat_amd import synth

@@ -57,7 +57,10 @@ extern "C" {
                       flag): chunkers with small windows (max_length below ~1 MB: the chain
                       does not fit beside the tile kernel) and batches below ~128 tiles of
                       16 KiB per tile-kernel wave (~8 GiB; the tile kernel's static schedule).
-                      RC_PIPE_ALL=1 in the environment pipelines every call. */
+                      RC_PIPE_ALL=1 in the environment pipelines every call.  The streams'
+                      bytes and the outputs must stay allocated until the call is waited for:
+                      a caching allocator (torch's) sees only the caller's stream, which a
+                      pipelined call's kernels do not run on. */
 
 typedef struct rc_chunker rc_chunker;
 

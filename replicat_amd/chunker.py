@@ -86,7 +86,8 @@ class GpuChunker:
 
         ``pipelined=True`` (RC_PIPELINED): the kernels run on the chunker's CU-partitioned
         streams, this call's chain beside the next call's tile kernel; ``stream`` orders the
-        inputs only, and ``wait(stream)`` orders the outputs."""
+        inputs only, and ``wait(stream)`` orders the outputs.  Keep the input and output
+        tensors alive until then: torch's caching allocator sees only ``stream``."""
         ptrs, lens = _ptr_array(ptrs), _ptr_array(lens)
         last = _ptr_array(last_piece if last_piece is not None else np.zeros(len(lens)))
         flags = (RC_OPEN if open_ else 0) | (RC_PIPELINED if pipelined else 0)
