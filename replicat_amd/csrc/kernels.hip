@@ -697,7 +697,11 @@ __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restri
         // retire the pending tile: (first maximal exact key, index) over its candidate lanes
 #ifndef RC_DIAG_NO_TAIL
         {
+#if defined(RC_DIAG_NO_EXACT)  // diagnostic build: no exact key (cost split; wrong records)
+            const uint64_t k = ((uint64_t)pend_hi << 32) | pend_lo;
+#else
             const uint64_t k = full_key(tl, th, pend_lo, pend_hi);
+#endif
             // a marker carries what the edge kernel needs: candidate lanes, ~stream
             const bool ptie = pend_st >> 31;
             const uint64_t pm = ptie ? 0 : pend_mask;
