@@ -550,7 +550,7 @@ class Config3ii:
         self.ends = None
         self.rounds = 0
 
-    def enqueue(self, w, entry, pipelined=False):
+    def enqueue(self, w, entry, pipelined=False, last=False):
         """Chunk window w from ``entry`` on the device (cut ends relative to entry in
         self.cuts / the returned tensor); enqueue only (pipelined: ch.wait orders the outputs)."""
         off = entry - w.start
@@ -564,7 +564,7 @@ class Config3ii:
         cuts = self.cuts if int(caps[0]) <= self.cap else self.be.zeros_i64(int(caps[0]))
         self.ch.chunk_device([src], [n], [max(0, w.last_piece - off) if not w.open else 0],
                              cuts.data_ptr(), self.counts.data_ptr(), self.hs, open_=w.open,
-                             pipelined=pipelined)
+                             pipelined=pipelined, last=last)
         self._tmp = tmp
         return cuts
 
@@ -576,7 +576,7 @@ class Config3ii:
 
     EXCHANGE = 64  # cut ends of each window's head and tail in the compact exchange
 
-    def step(self):
+    def step(self, last=False):
         """One GPU: the stream is chunked on the device and its cuts stay there.  Several: each
         rank chunks its window, and the ranks exchange only the first and last EXCHANGE cuts of
         their chains (a host gather of a few KB) to find where the true chain meets each
@@ -585,7 +585,8 @@ class Config3ii:
         self.ends, self._bounds = None, None
         # one rank: steps pipeline (nothing is read back between them); several: each step
         # reads its window's head and tail back, so its calls run in sequence
-        cuts = self.enqueue(self.w, self.w.start, pipelined=self.pipelined and self.world == 1)
+        cuts = self.enqueue(self.w, self.w.start, pipelined=self.pipelined and self.world == 1,
+                            last=last)
         self._cuts = cuts
         if self.world == 1:
             return
@@ -781,18 +782,20 @@ def main(argv=None, backend=Backend):
         lens_a = np.ascontiguousarray(lens, dtype=np.uint64)
         last_a = np.ascontiguousarray(last if last is not None else np.zeros(n), dtype=np.uint64)
 
-    def step(pipe=pipelined):
+    def step(pipe=pipelined, end=False):
+        # end: the last step of a pipelined run, whose chain has no tile kernel to hide behind
+        # (RC_PIPELINE_END: it runs on every CU)
         if long is not None:
             if pipe == pipelined:
-                long.step()
+                long.step(last=end)
             else:
                 long.enqueue(long.w, long.w.start, pipelined=pipe)
         else:
             ch.chunk_device(ptrs_a, lens_a, last_a, cuts.data_ptr(), counts.data_ptr(), hs,
-                            pipelined=pipe)
+                            pipelined=pipe, last=end)
 
-    for _ in range(args.warmup):
-        step()
+    for i in range(args.warmup):
+        step(end=i == args.warmup - 1)
     ch.wait(hs)
     be.synchronize()
     ranks.barrier()
@@ -800,8 +803,8 @@ def main(argv=None, backend=Backend):
     ch.timing(True)
     piped0 = ch.pipelined_calls()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    for i in range(args.steps):
+        step(end=i == args.steps - 1)
     ch.wait(hs)  # the outputs of every step (pipelined steps leave hs free)
     be.synchronize()
     ranks.barrier()

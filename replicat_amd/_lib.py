@@ -28,6 +28,7 @@ RC_ERR_OVERFLOW = 13
 RC_ERR_NO_DEVICE = 14
 RC_OPEN = 1
 RC_PIPELINED = 2
+RC_PIPELINE_END = 4
 RC_DIGEST_SLOT = 64
 
 # every symbol include/replicat_chunker.h, replicat_digest.h and replicat_cipher.h declare:

@@ -201,6 +201,7 @@ struct rc_chunker {
     uint32_t reserve_req = 0;  // rc_chunker_overlap / RC_OVERLAP_CUS (0: kDefaultReserve)
     uint32_t reserve = 0, tile_cus = 0;  // of the streams below (0: not created)
     hipStream_t tstream = nullptr, xstream = nullptr;
+    hipStream_t fstream = nullptr;  // RC_PIPELINE_END calls' edge and chain kernels: every CU
     hipEvent_t in_ev[2] = {nullptr, nullptr}, tiled[2] = {nullptr, nullptr};
     uint64_t pipelined_calls = 0;  // RC_PIPELINED requests that ran on the two streams
     bool overlap_failed = false;   // the masked streams could not be created (calls run in sequence)
@@ -414,7 +415,7 @@ constexpr uint64_t kLaneMinStreams = 256;
 
 int upload_and_launch(rc_chunker *ch, Workspace &ws, const Plan &plan, ChainParams prm,
                       uint64_t *d_cuts, int64_t *d_counts, hipStream_t stream,
-                      bool pipelined = false) {
+                      bool pipelined = false, bool end = false) {
     if (int rc = ws.d_desc.ensure(plan.bytes)) return rc;
     // records, then (small windows) the group maxima of every tile, then the tie lists
     if (int rc = ws.d_records.ensure(records_bytes(plan))) return rc;
@@ -436,9 +437,13 @@ int upload_and_launch(rc_chunker *ch, Workspace &ws, const Plan &plan, ChainPara
     hipStream_t ts = stream, xs = stream;
     if (pipelined) {
         ts = ch->tstream;
-        xs = ch->xstream;
+        // RC_PIPELINE_END: nothing follows for this chain to overlap, so it runs on every CU
+        xs = end ? ch->fstream : ch->xstream;
         HIP_TRY(hipEventRecord(ch->in_ev[wi], stream));
         HIP_TRY(hipStreamWaitEvent(ts, ch->in_ev[wi], 0));
+        // the chain kernels of consecutive calls stay in call order whichever stream they
+        // are on (calls may share output arrays): wait for the previous call's
+        HIP_TRY(hipStreamWaitEvent(xs, ch->ws[wi ^ 1].done, 0));
     }
     HIP_TRY(hipStreamWaitEvent(ts, ch->uploaded[wi], 0));
     const StreamDesc d = desc_view(ws.d_desc.p, plan.n);
@@ -526,6 +531,7 @@ int setup_overlap(rc_chunker *ch) {
     for (int i = 0; i < cus; ++i) ((uint32_t)i < want ? xm : tm)[i / 32] |= 1u << (i % 32);
     HIP_TRY(hipExtStreamCreateWithCUMask(&ch->tstream, (uint32_t)tm.size(), tm.data()));
     HIP_TRY(hipExtStreamCreateWithCUMask(&ch->xstream, (uint32_t)xm.size(), xm.data()));
+    if (!ch->fstream) HIP_TRY(hipStreamCreateWithFlags(&ch->fstream, hipStreamNonBlocking));
     for (int i = 0; i < 2; ++i) {
         if (!ch->in_ev[i]) HIP_TRY(hipEventCreateWithFlags(&ch->in_ev[i], hipEventDisableTiming));
         if (!ch->tiled[i]) HIP_TRY(hipEventCreateWithFlags(&ch->tiled[i], hipEventDisableTiming));
@@ -684,6 +690,7 @@ void rc_chunker_destroy(rc_chunker *ch) {
         if (ch->cstream) (void)hipStreamDestroy(ch->cstream);
         if (ch->tstream) (void)hipStreamDestroy(ch->tstream);
         if (ch->xstream) (void)hipStreamDestroy(ch->xstream);
+        if (ch->fstream) (void)hipStreamDestroy(ch->fstream);
         for (auto e : ch->uploaded)
             if (e) (void)hipEventDestroy(e);
         for (int i = 0; i < 2; ++i) {
@@ -830,7 +837,8 @@ int rc_chunk_device(rc_chunker *ch, uint64_t n, const uint8_t *const *d_streams,
                                    pipelined ? 16ull * ch->reserve : 0))
         return rc;
     return upload_and_launch(ch, ws, plan, chain_params(ch, plan, ~0ull, flags), d_cuts, d_counts,
-                             static_cast<hipStream_t>(hip_stream), pipelined);
+                             static_cast<hipStream_t>(hip_stream), pipelined,
+                             (flags & RC_PIPELINE_END) != 0);
 }
 
 int rc_chunker_overlap(rc_chunker *ch, uint32_t reserve_cus) {

@@ -124,9 +124,11 @@ def test_back_to_back_batches(pipe_all):
     for b, pool in enumerate(pools):
         cuts = torch.full((total,), -7, dtype=torch.int64, device='cuda')
         counts = torch.full((n,), -7, dtype=torch.int64, device='cuda')
-        # batches 3 and 6 run sequentially on the caller's stream between pipelined ones
+        # batches 3 and 6 run sequentially on the caller's stream between pipelined ones, and
+        # the last ends the sequence (RC_PIPELINE_END: its chain on every CU)
         ch.chunk_device(np.arange(n, dtype=np.uint64) * size + pool.data_ptr(), [size] * n, None,
-                        cuts.data_ptr(), counts.data_ptr(), _hs(), pipelined=b not in (3, 6))
+                        cuts.data_ptr(), counts.data_ptr(), _hs(), pipelined=b not in (3, 6),
+                        last=b == 7)
         outs.append((cuts, counts))
     ch.wait(_hs())
     got = [_ends(c, k, caps) for c, k in outs]
@@ -212,3 +214,32 @@ def test_full_size_pipelined(name, force, monkeypatch):
         assert G.cutlist_digest(ends) == g['sha256']
     del pool, outs
     torch.cuda.empty_cache()
+
+
+def test_pipeline_end_orders_shared_outputs(pipe_all):
+    """RC_PIPELINE_END calls (chain on every CU) between ordinary pipelined ones, all writing
+    the SAME output arrays from two different batches: the chains must stay in call order
+    across the two chain streams, so the arrays end with the last call's cuts."""
+    ch = GpuChunker(MIN_LENGTH, MAX_LENGTH, b'\xff' * 16)
+    n, size = 16, 16 * MIB
+    pools = []
+    for b in range(2):
+        pool = torch.empty(n * size + 64, dtype=torch.uint8, device='cuda')
+        fill_splitmix_streams(pool.data_ptr(), n, size, size, synth.DEFAULT_SEED, 500 * b, 1, _hs())
+        pools.append(pool)
+    total, caps = ch.capacity([size] * n)
+    exp = []
+    seq = GpuChunker(MIN_LENGTH, MAX_LENGTH, b'\xff' * 16)
+    for pool in pools:
+        exp.append(chunk_device(seq, [pool[i * size:(i + 1) * size] for i in range(n)], [size] * n))
+    assert exp[0] != exp[1]
+    cuts = torch.zeros(total, dtype=torch.int64, device='cuda')
+    counts = torch.zeros(n, dtype=torch.int64, device='cuda')
+    plan = [(0, False), (1, True), (0, False), (1, False), (0, True), (1, True), (0, False)]
+    for k in range(1, len(plan) + 1):
+        for b, end in plan[:k]:
+            ch.chunk_device(np.arange(n, dtype=np.uint64) * size + pools[b].data_ptr(), [size] * n,
+                            None, cuts.data_ptr(), counts.data_ptr(), _hs(), pipelined=True,
+                            last=end)
+        ch.wait(_hs())
+        assert _ends(cuts, counts, caps) == exp[plan[k - 1][0]], plan[:k]
