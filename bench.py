@@ -564,7 +564,7 @@ class Config3ii:
         cuts = self.cuts if int(caps[0]) <= self.cap else self.be.zeros_i64(int(caps[0]))
         self.ch.chunk_device([src], [n], [max(0, w.last_piece - off) if not w.open else 0],
                              cuts.data_ptr(), self.counts.data_ptr(), self.hs, open_=w.open,
-                             pipelined=pipelined, last=last)
+                             pipelined=pipelined, end=last)
         self._tmp = tmp
         return cuts
 
@@ -792,7 +792,7 @@ def main(argv=None, backend=Backend):
                 long.enqueue(long.w, long.w.start, pipelined=pipe)
         else:
             ch.chunk_device(ptrs_a, lens_a, last_a, cuts.data_ptr(), counts.data_ptr(), hs,
-                            pipelined=pipe, last=end)
+                            pipelined=pipe, end=end)
 
     for i in range(args.warmup):
         step(end=i == args.warmup - 1)

@@ -79,7 +79,7 @@ class GpuChunker:
         return int(total), caps
 
     def chunk_device(self, ptrs, lens, last_piece, cuts_ptr, counts_ptr, stream=0, open_=False,
-                     pipelined=False, last=False):
+                     pipelined=False, end=False):
         """Enqueue the chunking of device-resident streams (raw device pointers) on a HIP
         stream; cut END offsets land in the device array at ``cuts_ptr`` (u64, per-stream
         regions of ``capacity(lens)`` entries) and counts at ``counts_ptr`` (int64).
@@ -87,12 +87,12 @@ class GpuChunker:
         ``pipelined=True`` (RC_PIPELINED): the kernels run on the chunker's CU-partitioned
         streams, this call's chain beside the next call's tile kernel; ``stream`` orders the
         inputs only, and ``wait(stream)`` orders the outputs.  Keep the input and output
-        tensors alive until then: torch's caching allocator sees only ``stream``.  ``last``
+        tensors alive until then: torch's caching allocator sees only ``stream``.  ``end``
         (RC_PIPELINE_END): the end of a pipelined sequence -- the chain runs on every CU."""
         ptrs, lens = _ptr_array(ptrs), _ptr_array(lens)
         last = _ptr_array(last_piece if last_piece is not None else np.zeros(len(lens)))
         flags = ((RC_OPEN if open_ else 0) | (RC_PIPELINED if pipelined else 0)
-                 | (RC_PIPELINE_END if pipelined and last else 0))
+                 | (RC_PIPELINE_END if pipelined and end else 0))
         check(lib().rc_chunk_device(self._h, len(lens), ptrs.ctypes.data, lens.ctypes.data,
                                     last.ctypes.data, flags, cuts_ptr, counts_ptr, stream or None))
 

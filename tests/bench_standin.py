@@ -49,9 +49,8 @@ class OracleChunker:
         caps = np.array([int(L) // step + 3 for L in lens], dtype=np.uint64)
         return int(caps.sum()), caps
 
-    def chunk_device(self, ptrs, lens, last_piece, cuts_ptr, counts_ptr, stream=0, open_=False,
-                     pipelined=False, last=False):
-        last_call, last = last, last_piece  # GpuChunker's names: last_piece, last (end flag)
+    def chunk_device(self, ptrs, lens, last, cuts_ptr, counts_ptr, stream=0, open_=False,
+                     pipelined=False, end=False):
         self.pipelined_calls_n += bool(pipelined)
         _, caps = self.capacity(lens)
         base = np.concatenate([[0], np.cumsum(caps)[:-1]]).astype(np.int64)

@@ -128,7 +128,7 @@ def test_back_to_back_batches(pipe_all):
         # the last ends the sequence (RC_PIPELINE_END: its chain on every CU)
         ch.chunk_device(np.arange(n, dtype=np.uint64) * size + pool.data_ptr(), [size] * n, None,
                         cuts.data_ptr(), counts.data_ptr(), _hs(), pipelined=b not in (3, 6),
-                        last=b == 7)
+                        end=b == 7)
         outs.append((cuts, counts))
     ch.wait(_hs())
     got = [_ends(c, k, caps) for c, k in outs]
@@ -240,6 +240,6 @@ def test_pipeline_end_orders_shared_outputs(pipe_all):
         for b, end in plan[:k]:
             ch.chunk_device(np.arange(n, dtype=np.uint64) * size + pools[b].data_ptr(), [size] * n,
                             None, cuts.data_ptr(), counts.data_ptr(), _hs(), pipelined=True,
-                            last=end)
+                            end=end)
         ch.wait(_hs())
         assert _ends(cuts, counts, caps) == exp[plan[k - 1][0]], plan[:k]
