@@ -4,6 +4,7 @@ waves finish is the time a dynamic tile hand-out could recover at the end of the
 
     python -m replicat_amd.build --variant TSTAMPS -DRC_DIAG_TILE_STAMPS
     python scripts/tile_stamps.py [n_streams] [stream_mib] [min] [max]     (default: config 2)
+    python scripts/tile_stamps.py harness                                  (the reference harness)
 """
 import ctypes
 import json
@@ -19,15 +20,26 @@ import torch  # noqa: E402
 from replicat_amd import _lib, synth  # noqa: E402
 from replicat_amd.chunker import GpuChunker, fill_splitmix_streams  # noqa: E402
 
-n = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
-size = (int(sys.argv[2]) if len(sys.argv) > 2 else 64) << 20
-mn = int(sys.argv[3]) if len(sys.argv) > 3 else 128_000
-mx = int(sys.argv[4]) if len(sys.argv) > 4 else 5_120_000
-ch = GpuChunker(mn, mx, b'\xff' * 16)
-pool = torch.empty(n * size + 64, dtype=torch.uint8, device='cuda')
-ptrs = [pool.data_ptr() + i * size for i in range(n)]
 hs = torch.cuda.current_stream().cuda_stream
-fill_splitmix_streams(pool.data_ptr(), n, size, size, synth.DEFAULT_SEED, 0, 1, hs)
+last = None
+if len(sys.argv) > 1 and sys.argv[1] == 'harness':  # the reference harness's one 5.12 GB stream
+    pieces = list(synth.harness_buffers())
+    size = sum(len(p) for p in pieces)
+    pool = torch.empty(size + 64, dtype=torch.uint8, device='cuda')
+    off = 0
+    for p in pieces:
+        pool[off:off + len(p)].copy_(torch.frombuffer(p, dtype=torch.uint8))
+        off += len(p)
+    n, mn, mx, ptrs, last = 1, 128_000, 5_120_000, [pool.data_ptr()], [size - len(pieces[-1])]
+else:
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+    size = (int(sys.argv[2]) if len(sys.argv) > 2 else 64) << 20
+    mn = int(sys.argv[3]) if len(sys.argv) > 3 else 128_000
+    mx = int(sys.argv[4]) if len(sys.argv) > 4 else 5_120_000
+    pool = torch.empty(n * size + 64, dtype=torch.uint8, device='cuda')
+    ptrs = [pool.data_ptr() + i * size for i in range(n)]
+    fill_splitmix_streams(pool.data_ptr(), n, size, size, synth.DEFAULT_SEED, 0, 1, hs)
+ch = GpuChunker(mn, mx, b'\xff' * 16)
 total, caps = ch.capacity([size] * n)
 cuts = torch.zeros(total, dtype=torch.int64, device='cuda')
 counts = torch.zeros(n, dtype=torch.int64, device='cuda')
@@ -36,7 +48,7 @@ L.rc_diag_tile_read.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
 waves = torch.cuda.get_device_properties(0).multi_processor_count * 16
 for rep in range(4):
     ch.timing(True)
-    ch.chunk_device(ptrs, [size] * n, None, cuts.data_ptr(), counts.data_ptr(), hs)
+    ch.chunk_device(ptrs, [size] * n, last, cuts.data_ptr(), counts.data_ptr(), hs)
     torch.cuda.synchronize()
     ch.timing(False)
     tile_ms = ch.read_kernel_timing()[0]
