@@ -162,6 +162,7 @@ struct rc_chunker {
     bool small = false;   // window + 2 edge tiles within 64 tiles (the chain's one-row cache)
     bool groups = false;  // small windows: the tile kernel also writes per-group maxima
     uint64_t seg_force = 0, ext_steps = 4;  // segment-parallel chains (see stage_descriptors)
+    uint64_t seg_floor = 3;                 // shortest segment, in max_lengths
     uint64_t k0 = 0, k1 = 0;
     int device = 0;
     KeyTables tables;
@@ -340,7 +341,8 @@ int stage_descriptors(rc_chunker *ch, Workspace &ws, uint64_t n, const uint8_t *
         // batch of equal streams lands on one walker each when it already has enough streams
         uint64_t seg = ch->seg_force ? ch->seg_force
                                      : std::max<uint64_t>(total / kChainWalkers / 4 * 5 + 4, 1);
-        const uint64_t floor_len = ch->max_length < (1ull << 60) ? 3 * ch->max_length : ~0ull >> 2;
+        const uint64_t floor_len =
+            ch->max_length < (1ull << 60) ? ch->seg_floor * ch->max_length : ~0ull >> 2;
         if (!ch->seg_force) seg = std::max(seg, std::max<uint64_t>(floor_len, 4ull << 20));
         seg = std::max<uint64_t>((seg + 3) & ~3ull, 4);
         const uint64_t step = std::max<uint64_t>(4, (ch->min_length + 3) & ~3ull);
@@ -420,8 +422,9 @@ int upload_and_launch(rc_chunker *ch, Workspace &ws, const Plan &plan, ChainPara
     // records, then (small windows) the group maxima of every tile, then the tie lists
     if (int rc = ws.d_records.ensure(records_bytes(plan))) return rc;
     if (int rc = ws.d_scratch.ensure(std::max<uint64_t>(plan.scratch_entries, 1) * 8)) return rc;
-    // counts, merge points, slice offsets and slices of the parallel join (kernels.hip)
-    if (int rc = ws.d_seg_counts.ensure(std::max<uint64_t>(plan.n_segs, 1) * 32)) return rc;
+    // counts, merge points, slice offsets, slices and repaired counts of the parallel join
+    // (kernels.hip)
+    if (int rc = ws.d_seg_counts.ensure(std::max<uint64_t>(plan.n_segs, 1) * 40)) return rc;
     if (int rc = ensure_ctr(ws)) return rc;
     // The upload goes on the copy stream: stage_descriptors already waited for the call that
     // last used this workspace, so its device buffer is free now, while the previous call's
@@ -645,6 +648,8 @@ int rc_chunker_create(uint64_t min_length, uint64_t max_length, const uint8_t *k
         // the whole stream to the sequential join (0.58 ms instead of 0.13)
         ch->ext_steps = 4;
         if (const char *e = getenv("RC_SEGMENT_EXT")) ch->ext_steps = strtoull(e, nullptr, 0);
+        // RC_SEGMENT_FLOOR: the shortest segment in max_lengths (measurements)
+        if (const char *e = getenv("RC_SEGMENT_FLOOR")) ch->seg_floor = std::max<uint64_t>(strtoull(e, nullptr, 0), 1);
     }
     {
         DeviceGuard g(device);

@@ -1571,7 +1571,8 @@ __global__ __launch_bounds__(kChainWaves * 64) void rc_spec_kernel(const KeyTabl
                                                       uint64_t *__restrict__ cuts,
                                                       int64_t *__restrict__ counts,
                                                       uint64_t *__restrict__ scratch,
-                                                      uint64_t *__restrict__ seg_counts) {
+                                                      uint64_t *__restrict__ seg_counts,
+                                                      uint64_t *__restrict__ seg_rcount) {
     stage_chain_tables(tab);
     const uint32_t *pf = s_chain_lds;
     const uint64_t *full = reinterpret_cast<const uint64_t *>(s_chain_lds + 1024);
@@ -1635,8 +1636,14 @@ __global__ __launch_bounds__(kChainWaves * 64) void rc_spec_kernel(const KeyTabl
         pos = c1;
     }
     if (lane == 0) {
-        if (direct) counts[s] = overflow ? -1 : (int64_t)n;
-        else seg_counts[q] = overflow ? ~0ull : (n | (term ? (1ull << 63) : 0));
+        if (direct) {
+            counts[s] = overflow ? -1 : (int64_t)n;
+        } else {
+            // the count the scan reads, unless the merge kernel repairs (extends) this list
+            const uint64_t v = overflow ? ~0ull : (n | (term ? (1ull << 63) : 0));
+            seg_counts[q] = v;
+            seg_rcount[q] = v;
+        }
     }
 }
 
@@ -2343,55 +2350,139 @@ __global__ __launch_bounds__(256) void rc_quad_chain_kernel(const KeyTables *__r
 constexpr uint64_t kNoMerge = ~0ull;
 constexpr int64_t kNeedJoin = -2;
 
-__global__ __launch_bounds__(256) void rc_merge_kernel(StreamDesc d, uint64_t n_streams,
+// Repair (round 3): a boundary whose lists do not meet -- segment k-1's chain ran its
+// extension steps past g_k without landing on a cut of segment k's -- is no longer a reason to
+// walk the whole stream in sequence: the boundary's wave runs chain k-1 on from its last cut,
+// appending to list k-1 (its capacity is sized for min-length chunks, far more than a chain
+// needs), until a cut is g_k or one of list k's first 64 entries, or the chain ends or passes
+// list k's last entry (tests/test_join_model.py restates the whole splice on the CPU).  Boundaries
+// repair in parallel: each touches only its own list k-1 and writes the extended count to
+// seg_rcount[q - 1] (merge and repair of other boundaries read the original seg_counts).
+// Without a meeting within kRepairSteps the stream still takes the sequential join.
+constexpr int kRepairSteps = 64;
+
+template <int R>
+__global__ __launch_bounds__(256) void rc_merge_kernel(const KeyTables *__restrict__ tab,
+                                                       StreamDesc d, uint64_t n_streams,
                                                        ChainParams prm, uint64_t n_segs,
-                                                       const uint64_t *__restrict__ scratch,
+                                                       const TileRecord *__restrict__ rec,
+                                                       uint64_t *__restrict__ scratch,
                                                        const uint64_t *__restrict__ seg_counts,
-                                                       uint64_t *__restrict__ seg_merge) {
+                                                       uint64_t *__restrict__ seg_merge,
+                                                       uint64_t *__restrict__ seg_rcount,
+                                                       bool repair) {
     const uint32_t lane = lane_id();
     const uint64_t q = (uint64_t)blockIdx.x * (blockDim.x >> 6) +
                        __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (q >= n_segs) return;
-    const uint64_t s = find_index(d.seg_base, n_streams + 1, q);
-    const uint64_t sb = sload(d.seg_base + s), nseg = sload(d.seg_base + s + 1) - sb;
-    const uint64_t k = q - sb;
-    if (nseg <= 1 || k == 0) return;
-    const uint64_t *A = scratch + sload(d.scratch_base + s) + (k - 1) * prm.seg_cap;
-    const uint64_t *B = A + prm.seg_cap;
-    const uint64_t ca = seg_counts[q - 1], cb = seg_counts[q];
+    // no early return before the workgroup's barrier below: inactive waves just take part
+    bool active = q < n_segs;
+    uint64_t s = 0, k = 0, na = 0, nb = 0, g = 0, ca = ~0ull;
+    uint64_t *A = nullptr;
+    uint64_t bv = ~0ull, b_last = 0;
     uint64_t result = kNoMerge;
-    if (ca != ~0ull && cb != ~0ull) {
-        const uint64_t na = ca & ~(1ull << 63), nb = cb & ~(1ull << 63);
-        const uint64_t g = k * prm.seg_bytes;
-        // list k-1's entries at or past g are its last few (the chain's extension)
-        const uint64_t a0 = na > 64 ? na - 64 : 0;
-        const uint64_t ai = a0 + lane;
-        const uint64_t av = ai < na ? A[ai] : 0;
-        const uint64_t bv = lane < nb ? B[lane] : ~0ull;
-        const uint64_t b_last = lane_u64(bv, 63);
-        uint64_t cm = __ballot(ai < na && av >= g);
-        const bool whole = a0 == 0 || !(cm & 1ull);  // every entry >= g is in this window
-        for (; whole && cm; cm &= cm - 1) {
-            const int l = __builtin_ctzll(cm);
-            const uint64_t p = lane_u64(av, l);
-            if (p == g) {
-                result = (a0 + l + 1) | (0ull << 32);
-                break;
+    if (active) {
+        s = find_index(d.seg_base, n_streams + 1, q);
+        const uint64_t sb = sload(d.seg_base + s), nseg = sload(d.seg_base + s + 1) - sb;
+        k = q - sb;
+        active = nseg > 1 && k > 0;
+    }
+    if (active) {
+        A = scratch + sload(d.scratch_base + s) + (k - 1) * prm.seg_cap;
+        const uint64_t *B = A + prm.seg_cap;
+        ca = seg_counts[q - 1];
+        const uint64_t cb = seg_counts[q];
+        if (ca != ~0ull && cb != ~0ull) {
+            na = ca & ~(1ull << 63);
+            nb = cb & ~(1ull << 63);
+            g = k * prm.seg_bytes;
+            // list k-1's entries at or past g are its last few (the chain's extension)
+            const uint64_t a0 = na > 64 ? na - 64 : 0;
+            const uint64_t ai = a0 + lane;
+            const uint64_t av = ai < na ? A[ai] : 0;
+            bv = lane < nb ? B[lane] : ~0ull;
+            b_last = lane_u64(bv, 63);
+            uint64_t cm = __ballot(ai < na && av >= g);
+            const bool whole = a0 == 0 || !(cm & 1ull);  // every entry >= g is in this window
+            for (; whole && cm; cm &= cm - 1) {
+                const int l = __builtin_ctzll(cm);
+                const uint64_t p = lane_u64(av, l);
+                if (p == g) {
+                    result = (a0 + l + 1) | (0ull << 32);
+                    break;
+                }
+                const uint64_t hit = __ballot(bv == p);
+                if (hit) {
+                    result = (a0 + l + 1) | ((uint64_t)(__builtin_ctzll(hit) + 1) << 32);
+                    break;
+                }
+                if (nb > 64 && p > b_last) break;  // beyond the first 64 entries: let the walk do it
             }
-            const uint64_t hit = __ballot(bv == p);
-            if (hit) {
-                result = (a0 + l + 1) | ((uint64_t)(__builtin_ctzll(hit) + 1) << 32);
-                break;
-            }
-            if (nb > 64 && p > b_last) break;  // beyond the first 64 entries: let the walk do it
         }
     }
-    if (lane == 0) seg_merge[q] = result;
+    // repair only a live chain (not ended in list k-1) with a last cut to go on from, whose
+    // meeting can be seen in list k's first 64 entries
+    const bool need = active && result == kNoMerge && ca != ~0ull && (ca >> 63) == 0 && na > 0 &&
+                      nb <= 64 && repair;
+    if (__syncthreads_or(need)) {
+        stage_chain_tables(tab);
+        if (need) {
+            const uint32_t *pf = s_chain_lds;
+            const uint64_t *full = reinterpret_cast<const uint64_t *>(s_chain_lds + 1024);
+            const uint64_t *tl = full, *th = full + 1024;
+            const uint32_t lb_a = (lane & 31) * 4, lb_b = lb_a | 0x10000u;
+            const ChainStream st = chain_stream(d, s);
+            RecCache<R> cache;
+            uint64_t n = na, pos = A[na - 1];
+            // past list k's last entry the meeting is beyond what list k holds: give up there
+            // (the sequential join takes the stream)
+            const uint64_t b_end = nb ? lane_u64(bv, (int)nb - 1) : 0;
+            bool term = false, over = false, past = false;
+            for (int step = 0; step < kRepairSteps && result == kNoMerge && !over; ++step) {
+                if (pos >= st.L) {
+                    term = true;
+                    break;
+                }
+                uint64_t c[2] = {0, 0};
+                const int kind = chain_step<R>(tl, th, pf, rec, st, prm, cache, pos, lb_a, lb_b,
+                                               c[0], c[1]);
+                if (kind == kStepStop) {
+                    term = true;
+                    break;
+                }
+                const int nc = kind == kStepTail2 ? 2 : 1;
+                for (int e = 0; e < nc && result == kNoMerge; ++e) {
+                    if (n >= prm.seg_cap) {
+                        over = true;
+                        break;
+                    }
+                    if (lane == 0) A[n] = c[e];
+                    ++n;
+                    if (c[e] == g) {
+                        result = n;
+                        break;
+                    }
+                    const uint64_t hit = __ballot(bv == c[e]);
+                    if (hit) result = n | ((uint64_t)(__builtin_ctzll(hit) + 1) << 32);
+                    else if (c[e] > b_end) past = true;
+                }
+                if (past) break;
+                if (kind != kStepCut) {
+                    term = result == kNoMerge;  // the chain ended before the lists met
+                    break;
+                }
+                pos = c[0];
+            }
+            if (lane == 0 && !over) seg_rcount[q - 1] = n | (term ? (1ull << 63) : 0);
+            if (over) result = kNoMerge;
+        }
+    }
+    if (active && lane == 0) seg_merge[q] = result;
 }
 
 __global__ __launch_bounds__(256) void rc_scan_kernel(StreamDesc d, uint64_t n_streams,
                                                       const uint64_t *__restrict__ seg_counts,
                                                       const uint64_t *__restrict__ seg_merge,
+                                                      const uint64_t *__restrict__ seg_rcount,
                                                       uint64_t *__restrict__ seg_off,
                                                       uint64_t *__restrict__ seg_slice,
                                                       int64_t *__restrict__ counts) {
@@ -2403,20 +2494,44 @@ __global__ __launch_bounds__(256) void rc_scan_kernel(StreamDesc d, uint64_t n_s
     if (nseg <= 1) return;
     const uint64_t cap = sload(d.cut_cap + s);
     uint64_t carry = 0;
+    int64_t entry = 0;  // the true chain's entry index into the last segment of the previous 64
     bool fail = false, ended = false;
+    constexpr int64_t kNeg = INT64_MIN / 4;
     // every segment's slice is written (~0 past the chain's end): the copy kernel trusts it
     for (uint64_t k0 = 0; k0 < nseg; k0 += 64) {
         const uint64_t k = k0 + lane, q = sb + k;
         const bool valid = k < nseg;
-        const uint64_t c = valid ? seg_counts[q] : 0;
+        // a repaired list's extended count (its original count otherwise, see rc_spec_kernel)
+        const uint64_t c = valid ? seg_rcount[q] : 0;
         const uint64_t m_in = valid && k > 0 ? seg_merge[q] : 0;
         const uint64_t m_out = k + 1 < nseg ? seg_merge[q + 1] : kNoMerge;
         const uint64_t n_k = c & ~(1ull << 63);
         const bool term = (c >> 63) != 0 && c != ~0ull;
-        const uint64_t lo = m_in >> 32;
         const bool ends = m_out == kNoMerge;
         const uint64_t hi = ends ? n_k : (m_out & 0xffffffffu);
-        bool bad = valid && (c == ~0ull || m_in == kNoMerge || lo > hi || (ends && !term));
+        // Round 3: the entry into list k.  Boundary k says list k-1's first a_k entries lead to
+        // list k's entry b_k; a chain that enters list k-1 at e >= a_k is past that meeting, where
+        // the two lists are one chain, so it enters list k at b_k + (e - a_k) and takes nothing
+        // from list k-1 (a speculative chain whose extension ran past the next segment's merge).
+        // entry_k = max(b_k, entry_{k-1} + b_k - a_k): a max-plus recurrence, composed over the
+        // wave as pairs (P, Q) meaning x -> max(P, x + Q).
+        int64_t P = 0, Q = kNeg;  // segment 0: entry 0
+        if (valid && k > 0 && m_in != kNoMerge) {
+            P = (int64_t)(m_in >> 32);
+            Q = P - (int64_t)(m_in & 0xffffffffu);
+        }
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int64_t pp = __shfl_up(P, off), qp = __shfl_up(Q, off);
+            if (lane >= (uint32_t)off) {  // self after prev: x -> max(P, max(pp, x + qp) + Q)
+                P = max(P, pp + Q);
+                Q = max(qp + Q, kNeg);
+            }
+        }
+        const int64_t e_k = max(P, entry + Q);
+        const uint64_t lo = (uint64_t)e_k;
+        bool bad = valid && (c == ~0ull || (k > 0 && m_in == kNoMerge) ||
+                             (ends && (!term || lo > n_k)));
         // the chain reaches segment k only if no earlier segment ended it
         const uint64_t end_mask = ended ? 0 : __ballot(valid && ends && !bad);
         const uint64_t first_end = end_mask ? __builtin_ctzll(end_mask) : 64;
@@ -2426,7 +2541,7 @@ __global__ __launch_bounds__(256) void rc_scan_kernel(StreamDesc d, uint64_t n_s
             fail = true;
             break;
         }
-        uint64_t len = active ? hi - lo : 0, x = len;
+        uint64_t len = active && hi > lo ? hi - lo : 0, x = len;
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) {  // inclusive prefix sum over the wave
             const uint64_t y = __shfl_up(x, off);
@@ -2434,11 +2549,12 @@ __global__ __launch_bounds__(256) void rc_scan_kernel(StreamDesc d, uint64_t n_s
         }
         if (active) {
             seg_off[q] = carry + x - len;
-            seg_slice[q] = lo | (hi << 32);
+            seg_slice[q] = len ? (lo | (hi << 32)) : ~0ull;
         } else if (valid) {
             seg_slice[q] = ~0ull;
         }
         carry += lane_u64(x, 63);
+        entry = (int64_t)lane_u64((uint64_t)e_k, 63);
         if (end_mask) ended = true;
     }
     if (lane == 0) counts[s] = fail ? kNeedJoin : carry > cap ? -1 : (int64_t)carry;
@@ -2741,6 +2857,11 @@ bool rc_join_walk_only() {  // read per launch: tests switch it within one proce
     return e && e[0] == '1';
 }
 
+bool rc_repair_on() {  // RC_REPAIR=0: no repair (the round-2 fallback: any miss walks the stream)
+    const char *e = getenv("RC_REPAIR");
+    return !(e && e[0] == '0');
+}
+
 int cu_count() {
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 256;
@@ -2872,32 +2993,40 @@ int rc_launch_chain(const KeyTables *d_tables, StreamDesc desc, uint64_t n_strea
     // 4-wave workgroups on 20 KiB of LDS (compact tables)
     const bool small = prm.window / kTileKeys + 3 <= 64;  // window + both edge tiles in one row
     const uint64_t grid = (n_segs + kChainWaves - 1) / kChainWaves;
+    // d_seg_counts holds 5 arrays of n_segs: counts, merge points, slice offsets, slices and
+    // the repaired counts
+    uint64_t *seg_merge = d_seg_counts + n_segs, *seg_off = seg_merge + n_segs;
+    uint64_t *seg_slice = seg_off + n_segs, *seg_rcount = seg_slice + n_segs;
     if (small && prm.lean)
         hipLaunchKernelGGL((rc_spec_kernel<1, true>), dim3((unsigned)grid),
                            dim3(kChainWaves * kWaveSize), 0, st, d_tables, desc, n_streams, prm,
-                           n_segs, d_records, d_cuts, d_counts, d_scratch, d_seg_counts);
+                           n_segs, d_records, d_cuts, d_counts, d_scratch, d_seg_counts, seg_rcount);
     else if (small)
         hipLaunchKernelGGL((rc_spec_kernel<1, false>), dim3((unsigned)grid),
                            dim3(kChainWaves * kWaveSize), 0, st, d_tables, desc, n_streams, prm,
-                           n_segs, d_records, d_cuts, d_counts, d_scratch, d_seg_counts);
+                           n_segs, d_records, d_cuts, d_counts, d_scratch, d_seg_counts, seg_rcount);
     else
         hipLaunchKernelGGL((rc_spec_kernel<kRecUnroll, false>), dim3((unsigned)grid),
                            dim3(kChainWaves * kWaveSize), 0, st, d_tables, desc, n_streams, prm,
-                           n_segs, d_records, d_cuts, d_counts, d_scratch, d_seg_counts);
+                           n_segs, d_records, d_cuts, d_counts, d_scratch, d_seg_counts, seg_rcount);
     if (launch_status("rc_spec_kernel")) return 1;
     if (!any_multi) return 0;
-    // d_seg_counts holds 4 arrays of n_segs: counts, merge points, slice offsets, slices
-    uint64_t *seg_merge = d_seg_counts + n_segs, *seg_off = seg_merge + n_segs;
-    uint64_t *seg_slice = seg_off + n_segs;
     const uint64_t sgrid = (n_segs + 3) / 4, jgrid = (n_streams + kChainWaves - 1) / kChainWaves;
     if (!rc_join_walk_only()) {
-        hipLaunchKernelGGL(rc_merge_kernel, dim3((unsigned)sgrid), dim3(256), 0, st, desc,
-                           n_streams, prm, n_segs, (const uint64_t *)d_scratch,
-                           (const uint64_t *)d_seg_counts, seg_merge);
+        const bool repair = rc_repair_on();
+        if (small)
+            hipLaunchKernelGGL(rc_merge_kernel<1>, dim3((unsigned)sgrid), dim3(256), 0, st,
+                               d_tables, desc, n_streams, prm, n_segs, d_records, d_scratch,
+                               (const uint64_t *)d_seg_counts, seg_merge, seg_rcount, repair);
+        else
+            hipLaunchKernelGGL(rc_merge_kernel<kRecUnroll>, dim3((unsigned)sgrid), dim3(256), 0,
+                               st, d_tables, desc, n_streams, prm, n_segs, d_records, d_scratch,
+                               (const uint64_t *)d_seg_counts, seg_merge, seg_rcount, repair);
         if (launch_status("rc_merge_kernel")) return 1;
         hipLaunchKernelGGL(rc_scan_kernel, dim3((unsigned)jgrid), dim3(kChainWaves * kWaveSize), 0,
                            st, desc, n_streams, (const uint64_t *)d_seg_counts,
-                           (const uint64_t *)seg_merge, seg_off, seg_slice, d_counts);
+                           (const uint64_t *)seg_merge, (const uint64_t *)seg_rcount, seg_off,
+                           seg_slice, d_counts);
         if (launch_status("rc_scan_kernel")) return 1;
         hipLaunchKernelGGL(rc_copy_kernel, dim3((unsigned)sgrid), dim3(256), 0, st, desc,
                            n_streams, prm, n_segs, (const uint64_t *)d_scratch,

@@ -36,7 +36,13 @@ def _hs():
     return torch.cuda.current_stream().cuda_stream
 
 
-def test_reference_harness_stream():
+@pytest.mark.parametrize('seg', [None, (5_120_000, 1), (2 * 5_120_000, 0)])
+def test_reference_harness_stream(seg, monkeypatch):
+    """seg = (segment bytes, extension steps) forced: one-max segments with one extension step
+    (most boundaries repaired by the merge kernel), two-max segments with none."""
+    if seg is not None:
+        monkeypatch.setenv('RC_SEGMENT_BYTES', str(seg[0]))
+        monkeypatch.setenv('RC_SEGMENT_EXT', str(seg[1]))
     g = G.load('harness.json')
     assert (g['min'], g['max'], g['params']) == (MIN_LENGTH, MAX_LENGTH, None)
     L = g['length']

@@ -322,15 +322,19 @@ def test_tile_group_maxima_vs_oracle(kind):
         assert exact <= 2  # ties inside a lane are rare on random data
 
 
-@pytest.mark.parametrize('walk', ['0', '1'])
+@pytest.mark.parametrize('mode', ['repair', 'norepair', 'walk'])
 @pytest.mark.parametrize('seg_bytes,ext', [(1 << 16, 0), (1 << 16, 1), (1 << 16, 4),
-                                           (12 * 4096, 2), (1 << 20, 3)])
-def test_segmented_chains_vs_oracle(monkeypatch, seg_bytes, ext, walk):
+                                           (12 * 4096, 2), (1 << 20, 3), (1 << 12, 3)])
+def test_segmented_chains_vs_oracle(monkeypatch, seg_bytes, ext, mode):
     """Segment-parallel speculative chains + join, with tiny segments and short extensions
-    (ext 0 forces the join kernel to compute most steps itself); walk=1 sends every stream
-    through the sequential join instead of the parallel merge/scan/copy."""
+    (ext 0: most boundaries miss).  repair: the merge kernel runs a missing boundary's chain on
+    until the lists meet (the default); norepair (RC_REPAIR=0): any miss sends the stream to the
+    sequential join; walk (RC_JOIN_WALK=1): every stream through the sequential join.  4 KiB
+    segments are shorter than most chunks: extensions run past the next boundary's merge and
+    the scan's entry recurrence skips lists (tests/test_join_model.py restates the splice)."""
     o = _oracle()
-    monkeypatch.setenv('RC_JOIN_WALK', walk)
+    monkeypatch.setenv('RC_JOIN_WALK', '1' if mode == 'walk' else '0')
+    monkeypatch.setenv('RC_REPAIR', '0' if mode == 'norepair' else '1')
     monkeypatch.setenv('RC_SEGMENT_BYTES', str(seg_bytes))
     monkeypatch.setenv('RC_SEGMENT_EXT', str(ext))
     rnd = random.Random(seg_bytes + ext)
