@@ -161,8 +161,8 @@ struct rc_chunker {
     uint64_t min_length = 0, max_length = 0, window = 0;
     bool small = false;   // window + 2 edge tiles within 64 tiles (the chain's one-row cache)
     bool groups = false;  // small windows: the tile kernel also writes per-group maxima
-    uint64_t seg_force = 0, ext_steps = 4;  // segment-parallel chains (see stage_descriptors)
-    uint64_t seg_floor = 3;                 // shortest segment, in max_lengths
+    uint64_t seg_force = 0, ext_steps = 2;  // segment-parallel chains (see stage_descriptors)
+    uint64_t seg_floor = 2;                 // shortest segment, in max_lengths
     uint64_t k0 = 0, k1 = 0;
     int device = 0;
     KeyTables tables;
@@ -323,7 +323,8 @@ int stage_descriptors(rc_chunker *ch, Workspace &ws, uint64_t n, const uint8_t *
     std::copy(xt.begin(), xt.end(), u + 9 * n + 3);
     // Chain segments.  The chain of a stream is one wave walking ~(bound / chunk) steps; split
     // a stream only when the batch has too few streams to keep ~kChainWalkers waves busy, and
-    // never below 3 * max_length per segment (speculative chains must meet inside it).  4096
+    // never below seg_floor (2) * max_length per segment (speculative chains meet within a few
+    // chunks; the merge kernel repairs a boundary where they do not).  4096
     // walkers (4 waves per SIMD): a walker is latency-bound, so shorter chains on more waves
     // finish sooner even with the extension steps and the join (round 2, same box: config 2
     // 0.19 -> 0.15 ms, 3 (ii) 0.31 -> 0.20, config 4 0.47 -> 0.24; 1024 walkers before).
@@ -643,10 +644,14 @@ int rc_chunker_create(uint64_t min_length, uint64_t max_length, const uint8_t *k
         // chain segmentation knobs (RC_SEGMENT_BYTES forces a segment length; RC_SEGMENT_EXT
         // sets the speculative extension); the per-call choice is made in stage_descriptors
         if (const char *e = getenv("RC_SEGMENT_BYTES")) ch->seg_force = strtoull(e, nullptr, 0);
-        // 4 steps past the segment end: with 2, one of the harness stream's 332 segment
-        // boundaries (segments of 3 x max) failed to meet the next chain, and one failure sends
-        // the whole stream to the sequential join (0.58 ms instead of 0.13)
-        ch->ext_steps = 4;
+        // 2 steps past the segment end, segments of at least 2 x max (round 3, with boundary
+        // repair in the merge kernel: a boundary whose chains miss is continued where it is,
+        // where before one miss sent the whole stream to the sequential join, so round 2 ran 4
+        // steps over 3 x max).  One allocation each (scripts/chain_ab.py, profiles/r03/repair/):
+        // the harness's chain 0.108 -> 0.091 ms, 3 (ii) 0.241 -> 0.231, config 4 0.268 ->
+        // 0.253, config 2 0.159 -> 0.152; 1 x max segments with 1 step miss past the next
+        // list and fall back (1.76 ms on the harness)
+        ch->ext_steps = 2;
         if (const char *e = getenv("RC_SEGMENT_EXT")) ch->ext_steps = strtoull(e, nullptr, 0);
         // RC_SEGMENT_FLOOR: the shortest segment in max_lengths (measurements)
         if (const char *e = getenv("RC_SEGMENT_FLOOR")) ch->seg_floor = std::max<uint64_t>(strtoull(e, nullptr, 0), 1);
