@@ -412,6 +412,11 @@ int ensure_ctr(Workspace &ws) {
     return 0;
 }
 
+bool lean_pipe() {  // RC_PIPE_LEAN=0: the round-3 first version's extra event packets
+    const char *e = getenv("RC_PIPE_LEAN");
+    return !(e && e[0] == '0');
+}
+
 // batches of at least this many streams walk their chains one lane per stream (when the
 // windows are small and every stream is one segment: kernels.hip rc_lane_chain_kernel)
 constexpr uint64_t kLaneMinStreams = 256;
@@ -443,8 +448,14 @@ int upload_and_launch(rc_chunker *ch, Workspace &ws, const Plan &plan, ChainPara
         ts = ch->tstream;
         // RC_PIPELINE_END: nothing follows for this chain to overlap, so it runs on every CU
         xs = end ? ch->fstream : ch->xstream;
-        HIP_TRY(hipEventRecord(ch->in_ev[wi], stream));
-        HIP_TRY(hipStreamWaitEvent(ts, ch->in_ev[wi], 0));
+        // the inputs: nothing to wait for when the caller's stream has no work pending (each
+        // event record and wait is a packet between two tile kernels; RC_PIPE_LEAN=0 keeps them)
+        const char *lean = getenv("RC_PIPE_LEAN");
+        const bool lean_on = !(lean && lean[0] == '0');
+        if (!lean_on || hipStreamQuery(stream) != hipSuccess) {
+            HIP_TRY(hipEventRecord(ch->in_ev[wi], stream));
+            HIP_TRY(hipStreamWaitEvent(ts, ch->in_ev[wi], 0));
+        }
         // the chain kernels of consecutive calls stay in call order whichever stream they
         // are on (calls may share output arrays): wait for the previous call's
         HIP_TRY(hipStreamWaitEvent(xs, ch->ws[wi ^ 1].done, 0));
@@ -482,8 +493,9 @@ int upload_and_launch(rc_chunker *ch, Workspace &ws, const Plan &plan, ChainPara
     if (rc_launch_tiles(ch->d_tables, d, plan.n, plan.n_tiles,
                         static_cast<TileRecord *>(ws.d_records.p), grp, prm.hot, tie_lists(ws, plan),
                         static_cast<uint32_t *>(ws.d_ctr.p), ts, ch->timing ? ev[1] : nullptr,
-                        pipelined ? ch->tile_cus : 0u,
-                        xs, pipelined ? ch->tiled[wi] : nullptr))
+                        pipelined ? ch->tile_cus : 0u, xs,
+                        // the timing event after the tile kernel doubles as the hand-over event
+                        !pipelined ? nullptr : ch->timing && lean_pipe() ? ev[1] : ch->tiled[wi]))
         return fail(RC_ERR_HIP, "%s", rc_launch_error());
     if (ch->timing) HIP_TRY(hipEventRecord(ev[2], xs));
     if (rc_launch_chain(ch->d_tables, d, plan.n, prm, plan.n_segs,

@@ -2907,7 +2907,8 @@ int rc_launch_tiles(const KeyTables *d_tables, StreamDesc desc, uint64_t n_strea
     // the edge kernel's stream follows the tile kernel (also when there are no tiles)
     auto hand_over = [&]() -> int {
         if (est == st) return 0;
-        if (hipEventRecord((hipEvent_t)tiled, st) != hipSuccess ||
+        // `tiled` may be mid_event itself, already recorded after the tile kernel
+        if ((tiled != mid_event && hipEventRecord((hipEvent_t)tiled, st) != hipSuccess) ||
             hipStreamWaitEvent(est, (hipEvent_t)tiled, 0) != hipSuccess) {
             snprintf(g_launch_err, sizeof g_launch_err, "edge stream hand-over failed");
             return 1;

@@ -60,8 +60,10 @@ for r in range(rounds):
     order = settings if r % 2 == 0 else settings[::-1]
     for s in order:
         pipe = s != 'seq'
+        # pR:full -- the first version's extra event packets between tile kernels (RC_PIPE_LEAN=0)
+        os.environ['RC_PIPE_LEAN'] = '0' if s.endswith(':full') else '1'
         if pipe:
-            ch.overlap(int(s[1:]))
+            ch.overlap(int(s[1:].split(':')[0]))
 
         def step():
             ch.chunk_device(ptrs, lens, last, cuts.data_ptr(), counts.data_ptr(), hs,
