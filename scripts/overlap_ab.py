@@ -5,6 +5,7 @@ median wall time per step over K back-to-back steps, the tile kernel's HIP-event
 edge + chain time are printed.  Every setting must give the same cut lists.
 
     python scripts/overlap_ab.py [config] [rounds] [setting ...]   setting = seq | pR (R CUs)
+                                          [:full] [@STATIC:CHUNK] (tile schedule, per launch)
     python scripts/overlap_ab.py 2 4 seq p8 p16 p32
 """
 import json
@@ -59,11 +60,17 @@ res = {s: [] for s in settings}
 for r in range(rounds):
     order = settings if r % 2 == 0 else settings[::-1]
     for s in order:
-        pipe = s != 'seq'
+        base, _, sched = s.partition('@')  # ...@STATIC:CHUNK -- the tile schedule (per launch)
+        if sched:
+            os.environ['RC_TILE_STATIC'], os.environ['RC_TILE_CHUNK'] = sched.split(':')
+        else:
+            os.environ.pop('RC_TILE_STATIC', None)
+            os.environ.pop('RC_TILE_CHUNK', None)
+        pipe = base != 'seq'
         # pR:full -- the first version's extra event packets between tile kernels (RC_PIPE_LEAN=0)
-        os.environ['RC_PIPE_LEAN'] = '0' if s.endswith(':full') else '1'
+        os.environ['RC_PIPE_LEAN'] = '0' if base.endswith(':full') else '1'
         if pipe:
-            ch.overlap(int(s[1:].split(':')[0]))
+            ch.overlap(int(base[1:].split(':')[0]))
 
         def step():
             ch.chunk_device(ptrs, lens, last, cuts.data_ptr(), counts.data_ptr(), hs,
