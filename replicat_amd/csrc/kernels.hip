@@ -523,7 +523,7 @@ __device__ uint64_t g_tile_stamp[3 * 8192];
 // gave every wave the same static share and measured (RC_DIAG_TILE_STAMPS) the waves of one
 // launch ending between 52 % and 100 % of its time: the slowest waves' tail was ~23 % of the
 // kernel.  Small launches (fewer than kDynMinPerWave tiles per wave) stay fully static.
-// Static share 25 %, then units of 12 tiles (32 until late round 3; tile_units): 10-11 % faster on configs 2,
+// Static share 10 %, then units of 12 tiles (25 % and 32 until late round 3; tile_units): 10-11 % faster on configs 2,
 // 3 (iii) and 4 than fully static on the same allocation.
 struct TileUnits {  // tile indices fit 32 bits (the tie lists store them as u32)
     uint32_t n_tiles, nw, s0, chunk, dyn0, n_units;
@@ -540,7 +540,7 @@ struct TileUnits {  // tile indices fit 32 bits (the tie lists store them as u32
     }
 };
 
-// Units of a launch over n_tiles tiles by nw waves.  RC_TILE_STATIC (per mille, default 250): the
+// Units of a launch over n_tiles tiles by nw waves.  RC_TILE_STATIC (per mille, default 100): the
 // share of the tiles handed out statically; RC_TILE_CHUNK (default 12): dynamic unit size.  Both
 // measured on one allocation per config (scripts/tile_sched_ab.py, profiles/r03/sched): tile
 // kernel vs the round-2 fully static schedule, config 2 11.06 -> 9.88 ms, 3 (iii) 11.46 -> 10.32,
@@ -550,13 +550,15 @@ struct TileUnits {  // tile indices fit 32 bits (the tie lists store them as u32
 // 10.17 / 10.21 ms with 32, 9.87 / 9.89 with 12, 9.82 with 10, 9.90 / 9.87 with 8 -- and 10.51
 // with 6: every grab is a device-scope atomic on one counter, and ~480 k of them in a 10 ms
 // launch saturate it.  12 keeps half that rate (3 ii 10.65 -> 10.41 ms, 3 iii and config 4 ~1 %).
+// With 12-tile units a 10 % static share beat 25 % (config 2 9.77 -> 9.68 ms pipelined, 9.78 ->
+// 9.68 sequential, 3 iii 9.98 -> 9.94; 0 %: 9.72; profiles/r03/sched_static/): ~290 k grabs.
 constexpr uint64_t kDynMinPerWave = 128;  // fewer tiles per wave: one static unit each
 constexpr uint64_t kDynChunkMin = 2;    // units of at least 2 tiles
 __host__ inline TileUnits tile_units(uint64_t n_tiles, uint64_t nw) {
     TileUnits U;
     U.n_tiles = (uint32_t)n_tiles;
     U.nw = (uint32_t)nw;
-    uint64_t permille = 250, chunk = 12, dyn_min = kDynMinPerWave;
+    uint64_t permille = 100, chunk = 12, dyn_min = kDynMinPerWave;
     if (const char *e = getenv("RC_TILE_STATIC")) permille = strtoull(e, nullptr, 0);
     if (const char *e = getenv("RC_TILE_CHUNK")) chunk = strtoull(e, nullptr, 0);
     // RC_TILE_DYN_MIN (tests): the tiles per wave from which units are dynamic
