@@ -523,8 +523,9 @@ __device__ uint64_t g_tile_stamp[3 * 8192];
 // gave every wave the same static share and measured (RC_DIAG_TILE_STAMPS) the waves of one
 // launch ending between 52 % and 100 % of its time: the slowest waves' tail was ~23 % of the
 // kernel.  Small launches (fewer than kDynMinPerWave tiles per wave) stay fully static.
-// Static share 10 %, then units of 12 tiles (25 % and 32 until late round 3; tile_units): 10-11 % faster on configs 2,
-// 3 (iii) and 4 than fully static on the same allocation.
+// Static share 25 % and 32-tile units: 10-11 % faster on configs 2, 3 (iii) and 4 than fully
+// static on the same allocation; late in round 3, 10 % and 12-tile units took ~4 % more off
+// (tile_units).
 struct TileUnits {  // tile indices fit 32 bits (the tie lists store them as u32)
     uint32_t n_tiles, nw, s0, chunk, dyn0, n_units;
     __device__ __host__ void range(uint32_t u, uint32_t &b, uint32_t &e) const {
