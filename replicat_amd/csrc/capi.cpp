@@ -546,7 +546,12 @@ int setup_overlap(rc_chunker *ch) {
     std::vector<uint32_t> tm((cus + 31) / 32, 0u), xm((cus + 31) / 32, 0u);
     for (int i = 0; i < cus; ++i) ((uint32_t)i < want ? xm : tm)[i / 32] |= 1u << (i % 32);
     HIP_TRY(hipExtStreamCreateWithCUMask(&ch->tstream, (uint32_t)tm.size(), tm.data()));
-    HIP_TRY(hipExtStreamCreateWithCUMask(&ch->xstream, (uint32_t)xm.size(), xm.data()));
+    const hipError_t ex = hipExtStreamCreateWithCUMask(&ch->xstream, (uint32_t)xm.size(), xm.data());
+    if (ex != hipSuccess) {  // both streams or neither (a call checks tstream only)
+        (void)hipStreamDestroy(ch->tstream);
+        ch->tstream = ch->xstream = nullptr;
+        return fail(RC_ERR_HIP, "hipExtStreamCreateWithCUMask failed: %s", hipGetErrorString(ex));
+    }
     if (!ch->fstream) HIP_TRY(hipStreamCreateWithFlags(&ch->fstream, hipStreamNonBlocking));
     for (int i = 0; i < 2; ++i) {
         if (!ch->in_ev[i]) HIP_TRY(hipEventCreateWithFlags(&ch->in_ev[i], hipEventDisableTiming));
