@@ -169,3 +169,20 @@ def test_world_size_must_match_gpus():
     line, rc, err = _cli(['--gpus', '2'] + SMALL, WORLD_SIZE='1', RANK='0', LOCAL_RANK='0')
     assert rc == 3 and line is None
     assert '--gpus 2' in err
+
+
+def test_pipelined_line_fields():
+    """The default line: steps are pipelined requests (RC_PIPELINED), the reserve and the
+    number that overlapped are reported with the same steps' unpipelined time, and the roofline
+    says what its edge / chain times mean then; --pipeline off reports plain sequential steps."""
+    line, rc, err = _cli(['--gpus', '1'] + SMALL[:-10] + ['--steps', '3', '--warmup', '1']
+                         + SMALL[-6:])
+    assert rc == 0, err[-2000:]
+    p = line['pipeline']
+    assert p['on'] is True and p['reserve_cus'] == 32 and p['pipelined_steps'] == 3
+    assert p['unpipelined_ms_per_step'] is not None and 'every step still computes' in p['note']
+    assert 'pipelined steps' in line['roofline']['timing_note']
+    line, rc, err = _cli(['--gpus', '1', '--pipeline', 'off'] + SMALL)
+    assert rc == 0, err[-2000:]
+    assert line['pipeline'] == {'on': False}
+    assert 'timing_note' not in line['roofline']
