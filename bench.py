@@ -19,9 +19,12 @@ one-GPU rehearsal), and then the roofline is null (the ranks' HIP events time ea
 Ranks shard the work per stream (config 2: stream ids rank*1024 ..; config 4: stream i on
 GPU i mod 8) with no data-path collective: "scaling": "weak".  The process group is gloo and
 carries only the barriers, the max-over-ranks time and the parity flags -- never stream data.
-Rank 0 prints one JSON line.  Parity is checked in-run against the reference's cut-list
-digests (tests/golden: config 2 (key ff, and the seeded key's first 128 streams), 3 (i),
-3 (ii), 3 (iii), 4 on every rank, 5, harness).
+Rank 0 prints one JSON line.  Parity is checked in-run by EVERY rank against the reference's
+cut-list digests of that rank's own shard (tests/golden/ranks.json for ranks 0..7: config 2
+with key ff and the seeded key's first 128 streams, 3 (iii), 5; config4.json; the harness;
+3 (i) by its closed form; 3 (ii) for the stream lengths large.json / ranks.json hold); the
+line's flag is the AND over ranks, null when any rank has no fixture.  The CPU baseline runs
+on rank 0 over N x the per-GPU host-core share.
 
 `--config harness` is the reference's own benchmark (Repository._benchmark_chunker,
 /root/reference/replicat/repository.py:1984-2008): 10 x 512,000,000 Random(0) bytes as one
@@ -282,13 +285,14 @@ def bytes_needed(max_length, lens, last):
 
 # ------------------------------------------------------------------------ CPU baseline
 
-def cpu_share():
-    """(cores to use, cores in the affinity mask): the mask, capped by the CPU share the GPU box
-    grants one GPU (OMP_NUM_THREADS there; nproc and the mask show the whole machine)."""
+def cpu_share(world=1):
+    """(cores to use, cores in the affinity mask): the mask, capped by the CPU share the node
+    grants the line's GPUs -- OMP_NUM_THREADS per GPU there (nproc and the mask show the whole
+    machine), times the ranks, so an N-GPU line is set against N GPUs' host cores."""
     n = len(os.sched_getaffinity(0))
     cap = os.environ.get('OMP_NUM_THREADS')
     if cap and cap.isdigit() and int(cap) > 0:
-        return min(n, int(cap)), n
+        return min(n, int(cap) * max(1, world)), n
     return n, n
 
 
@@ -466,7 +470,9 @@ class Config5:
         ch.chunk_device([base + i * slot for i in range(n)], olens, None, ocuts.data_ptr(),
                         ocounts.data_ptr(), hs)
         self.orig_digest, _, self.orig_ends = cut_digest(ocuts, ocounts, ocaps)
-        plan = synth.edit_plan(n, n // 2, size) if rank == 0 and n == 1024 else []
+        # every rank edits its own shard: rank 0 the single-GPU plan (seed 5), rank r seed 5 + r
+        # (tests/golden/make_golden.py rank_edit_plan; ranks.json holds each rank's reference)
+        plan = synth.edit_plan(n, n // 2, size, seed=5 + rank) if n == 1024 else []
         self.plan = {sid: (kind, off, payload) for sid, kind, off, payload in plan}
         self.edited = sorted(self.plan)
         self.buf = torch.empty(n * slot + 64, dtype=torch.uint8, device=device)
@@ -625,47 +631,75 @@ def _golden():
 
 
 def check_parity(args, n, size, rank, long, edit, ends, digest):
-    """(flag, scope) of this rank's cut lists against the reference's digests, or (None, None)
-    when no fixture covers the workload."""
+    """(flag, scope) of THIS rank's cut lists against the reference's digests of this rank's
+    own shard (tests/golden/ranks.json: every rank of an up-to-8-GPU line; rank 0's entries are
+    the single-GPU fixtures), or (None, None) when no fixture covers the workload.  main() ANDs
+    the ranks' flags into the line's (null when any rank has none)."""
     G = _golden()
-    gold = {d['name']: d for d in G.load('digests.json')}
+    R = G.load('ranks.json')
     ff = args.key == 'ff'
-    if args.config == '2' and ff and n == 1024 and size == 64 << 20 and rank == 0:
-        return digest == gold['config2_ff']['sha256'], 'rank 0 (streams 0..1023)'
-    if args.config == '2' and not ff and n >= 128 and size == 64 << 20 and rank == 0:
+    mine = rank < R['ranks']
+    c2 = size == 64 << 20 and n == 1024
+    if args.config == '2' and ff and c2 and mine:
+        g = R['config2_ff'][rank]
+        return digest == g['sha256'], f'streams {g["first_id"]}..{g["first_id"] + n - 1}'
+    small = R.get('small')
+    if args.config == '2' and ff and mine and small and (n, size) == (small['streams'], small['size']):
+        # a small config-2-shaped shard (the CPU tests' stand-in checks every rank against it)
+        g = small['per_rank'][rank]
+        return digest == g['sha256'], f'streams {g["first_id"]}..{g["first_id"] + n - 1}'
+    if args.config == '2' and not ff and c2 and mine:
         # an encrypted repository's key (repository.py:174-181): the reference cut the first
-        # 128 streams with synth.seeded_key(1) (tests/golden/make_golden.py)
-        g = gold['config2_seeded_first128']
+        # 128 streams of every shard with synth.seeded_key(1) (tests/golden/make_golden.py)
+        g = R['config2_seeded'][rank]
         from replicat_amd import synth
         assert synth.seeded_key(1).hex() == g['params']
-        return (G.cutlist_digest(ends[:128]) == g['sha256'],
-                'rank 0, seeded key: streams 0..127')
-    if args.config == '3iii' and ff and rank == 0 and n == 65536:
-        return digest == gold['config3iii']['sha256'], 'all 65536 streams'
+        k = g['streams']
+        return (G.cutlist_digest(ends[:k]) == g['sha256'],
+                f'seeded key: streams {g["first_id"]}..{g["first_id"] + k - 1}')
+    if args.config == '3iii' and ff and n == 65536 and mine:
+        g = R['config3iii'][rank]
+        return digest == g['sha256'], f'all 65536 streams ({g["first_id"]}..)'
     if args.config == '3iii' and ff and rank == 0 and n >= 4096:
+        gold = {d['name']: d for d in G.load('digests.json')}
         return (G.cutlist_digest(ends[:4096]) == gold['config3iii_first4096']['sha256'],
                 'first 4096 streams')
-    if args.config == '3i' and ff and rank == 0:
+    if args.config == '3i' and ff:
         # the tail rule alone: one chunk per stream (adapters.cpp:50-51)
         return all(len(e) == 1 and int(e[0]) == size for e in ends), 'every stream'
-    if long is not None and ff and long.L == 64 << 30:
-        large = {d['name']: d for d in G.load('large.json')}
-        return digest == large['config3ii']['sha256'], 'the whole stream'
+    if long is not None and ff:
+        # one stream split over the ranks: every rank holds the whole spliced list
+        for g in [d for d in G.load('large.json') if d['name'] == 'config3ii'] + R.get('config3ii', []):
+            if long.L == g['size'] and long.P == g['last_piece']:
+                return digest == g['sha256'], f'the whole {long.L >> 30} GiB stream'
+        return None, None
     if args.config == '4' and ff and n == 16 and size == 8 << 30 and rank < 8:
         c4 = G.load('config4.json')
-        return digest == c4['per_gpu'][rank]['sha256'], 'every rank: streams r, r + 8, ..'
+        return digest == c4['per_gpu'][rank]['sha256'], 'streams r, r + 8, ..'
     if args.config == 'harness':
         return digest == G.load('harness.json')['sha256'], 'the whole harness stream'
-    if edit is not None and ff and n == 1024 and size == 64 << 20 and rank == 0:
-        large = {d['name']: d for d in G.load('large.json')}
+    if edit is not None and ff and c2 and mine:
         dedup = edit.result = edit.dedup(ends)
-        g5 = large['config5']
+        g5 = R['config5'][rank]
         return ((G.cutlist_digest([ends[i] for i in edit.edited]) == g5['edited_sha256']
                  and edit.orig_digest == g5['original_sha256']
                  and dedup['dup_bytes_edited'] == g5['dup_bytes_edited']
                  and dedup['total_bytes_edited'] == g5['total_bytes_edited']),
-                'rank 0 (512 edited streams + dedup)')
+                f'{len(edit.edited)} edited streams of the shard + dedup')
     return None, None
+
+
+def line_parity(per_rank, world):
+    """The line's flag: the AND over every rank's own check, null when any rank has no fixture
+    (a line whose cut lists were not all compared must not read true)."""
+    flags = [r['parity'] for r in per_rank]
+    if len(flags) == 1:
+        return flags[0], per_rank[0]['parity_scope']
+    if any(f is None for f in flags):
+        unchecked = [r['rank'] for r in per_rank if r['parity'] is None]
+        return None, f'no fixture for rank(s) {unchecked}'
+    return all(flags), f'every rank ({world}) against its own shard: ' + '; '.join(
+        f'rank {r["rank"]}: {r["parity_scope"]}' for r in per_rank)
 
 
 def roofline(bytes_per_step, read, tile_avg, edge_avg, chain_avg, traffic, traffic_src, bid):
@@ -847,11 +881,9 @@ def main(argv=None, backend=Backend):
         be.synchronize()
         seq_ms = (time.perf_counter() - t1) * 1e3 / seq
     mine['parity'] = parity
+    mine['parity_scope'] = scope
     per_rank = ranks.gather(mine)
-    flags = [r['parity'] for r in per_rank]
-    if args.config == '4' and all(f is not None for f in flags):
-        parity = all(flags)  # every rank checked its own shard
-        scope = f'{len(flags)} rank(s), each its own 16 streams'
+    parity, scope = line_parity(per_rank, world)
     for r, d in zip(per_rank, devices):
         r.update(device=d['device'], pci=d['pci'], uuid=d['uuid'])
 
@@ -877,14 +909,15 @@ def main(argv=None, backend=Backend):
         # the CPU leg runs on rank 0 after the timed region, at every N (the other ranks wait
         # at the final barrier); its sample is rank 0's own streams
         if args.key == 'ff' and args.config == '2' and args.cpu_streams != 0:
-            procs, seen = cpu_share()
+            procs, seen = cpu_share(world)
             procs = args.cpu_procs or procs
             sample = min(args.cpu_streams or n, n)
             cpu, cpu_ends = cpu_baseline(sample, size, synth.DEFAULT_SEED, procs)
             cpu['affinity_cores'] = seen
             cpu['cores_basis'] = (
-                f'{procs} = min(affinity mask {seen}, OMP_NUM_THREADS) -- the host-core share '
-                f'the GPU box grants each GPU (OMP_NUM_THREADS; nproc and the mask show the whole '
+                f'{procs} = min(affinity mask {seen}, {world} GPU(s) x OMP_NUM_THREADS '
+                f'{os.environ.get("OMP_NUM_THREADS")}) -- the host-core share the node grants '
+                f'the line\'s GPUs (OMP_NUM_THREADS per GPU; nproc and the mask show the whole '
                 f"machine); --cpu-procs overrides" if os.environ.get('OMP_NUM_THREADS')
                 else f'{procs} = the affinity mask')
             if ends is not None:

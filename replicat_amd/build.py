@@ -22,7 +22,8 @@ CSRC = os.path.join(HERE, 'csrc')
 LIB = os.path.join(HERE, 'libreplicat_chunker.so')
 SOURCES = [os.path.join(CSRC, n) for n in ('kernels.hip', 'capi.cpp', 'blake2b.hip', 'capi_digest.cpp', 'gcm.hip',
                                              'capi_cipher.cpp')]
-HEADERS = [os.path.join(CSRC, n) for n in ('gclmul.h', 'digest_kernels.h', 'capi_internal.h', 'cipher_kernels.h')] + [
+HEADERS = [os.path.join(CSRC, n) for n in ('gclmul.h', 'digest_kernels.h', 'capi_internal.h', 'cipher_kernels.h',
+                                             'knobs.h', 'diag.h')] + [
     os.path.join(ROOT, 'include', n) for n in ('replicat_chunker.h', 'replicat_digest.h', 'replicat_cipher.h')]
 ARCH = 'gfx950'
 # -amdgpu-atomic-optimizer-strategy=None: the tile kernel's one-lane grab of its next work unit

@@ -17,6 +17,7 @@
 #include "../../include/replicat_chunker.h"
 #include "capi_internal.h"
 #include "gclmul.h"
+#include "knobs.h"
 
 using namespace rc;
 
@@ -157,6 +158,52 @@ int rc_fail(int code, const char *fmt, ...) {
     return code;
 }
 
+namespace {
+
+// The live-handle registry (capi_internal.h).  Heap-allocated and never freed: a static
+// container would have a destructor of its own in the exit sequence.
+struct LiveHandle {
+    void *h;
+    void (*destroy)(void *);
+};
+std::mutex g_live_mu;
+std::vector<LiveHandle> *g_live = nullptr;
+bool g_exiting = false;
+
+void destroy_live_at_exit() {
+    std::vector<LiveHandle> left;
+    {
+        std::lock_guard<std::mutex> lock(g_live_mu);
+        g_exiting = true;
+        if (g_live) left.swap(*g_live);
+    }
+    for (auto it = left.rbegin(); it != left.rend(); ++it) it->destroy(it->h);
+}
+
+}  // namespace
+
+void rc_track(void *handle, void (*destroy)(void *)) {
+    std::lock_guard<std::mutex> lock(g_live_mu);
+    if (!g_live) {
+        g_live = new std::vector<LiveHandle>();
+        // registered after the HIP runtime initialised (the caller created a device object
+        // first), so it runs before the runtime's own exit-time teardown
+        std::atexit(destroy_live_at_exit);
+    }
+    g_live->push_back({handle, destroy});
+}
+
+void rc_untrack(void *handle) {
+    std::lock_guard<std::mutex> lock(g_live_mu);
+    if (!g_live || g_exiting) return;
+    for (size_t i = 0; i < g_live->size(); ++i)
+        if ((*g_live)[i].h == handle) {
+            (*g_live)[i] = g_live->back();
+            g_live->pop_back();
+            return;
+        }
+}
+
 struct rc_chunker {
     uint64_t min_length = 0, max_length = 0, window = 0;
     bool small = false;   // window + 2 edge tiles within 64 tiles (the chain's one-row cache)
@@ -165,6 +212,8 @@ struct rc_chunker {
     uint64_t seg_floor = 2;                 // shortest segment, in max_lengths
     uint64_t k0 = 0, k1 = 0;
     int device = 0;
+    Knobs knobs;      // knobs.h, read once at creation
+    TileSched sched;  // the tile kernel's schedule (from knobs)
     KeyTables tables;
     KeyTables *d_tables = nullptr;
     std::mutex mu;  // one call at a time per chunker (the reference is used by one thread)
@@ -177,9 +226,11 @@ struct rc_chunker {
         DevBuf d_scratch;   // speculative chain lists of multi-segment streams
         DevBuf d_seg_counts;  // one count (+ termination bit) per chain segment
         DevBuf d_ctr;         // the tile kernel's grab counter (zeroed once, then by the edge kernel)
+        bool ctr_dirty = false;  // a launch failed between the tile and the edge kernel: re-zero it
         std::vector<uint64_t> xtiles;  // host list of the tiles the fast path does not take
         hipEvent_t done = nullptr;  // the call that last used this workspace has finished
         bool pending = false;
+        bool piped = false;  // that call's chain ran on a pipelined stream, not the caller's
     } ws[2];
     unsigned next_ws = 0;
 
@@ -199,7 +250,7 @@ struct rc_chunker {
     // RC_PIPELINED calls (overlap mode): the tile kernel on `tstream`, whose CU mask leaves out
     // `reserve` CUs, the edge and chain kernels on `xstream`, masked to exactly those CUs, so
     // that one call's chain runs beside the next call's tile kernel
-    uint32_t reserve_req = 0;  // rc_chunker_overlap / RC_OVERLAP_CUS (0: kDefaultReserve)
+    uint32_t reserve_req = 0;  // rc_chunker_overlap (0: RC_OVERLAP_CUS, default 32)
     uint32_t reserve = 0, tile_cus = 0;  // of the streams below (0: not created)
     hipStream_t tstream = nullptr, xstream = nullptr;
     hipStream_t fstream = nullptr;  // RC_PIPELINE_END calls' edge and chain kernels: every CU
@@ -404,17 +455,31 @@ size_t records_bytes(const Plan &plan) {
            rc_tie_list_words(plan.n_tiles) * 4;
 }
 
-// the grab counter: allocated and zeroed once per workspace; every edge kernel leaves it 0
-int ensure_ctr(Workspace &ws) {
-    if (ws.d_ctr.p) return 0;
-    if (int rc = ws.d_ctr.ensure(256)) return rc;
-    HIP_TRY(hipMemset(ws.d_ctr.p, 0, 256));
+// the grab counter: allocated and zeroed once per workspace; every edge kernel leaves it 0.  A
+// launch that failed after its tile kernel was queued leaves it dirty (abandon_launch): it is
+// zeroed again on the stream of the next tile kernel, after the host has waited for the orphan.
+int ensure_ctr(Workspace &ws, hipStream_t st) {
+    if (!ws.d_ctr.p) {
+        if (int rc = ws.d_ctr.ensure(256)) return rc;
+        HIP_TRY(hipMemset(ws.d_ctr.p, 0, 256));
+        ws.ctr_dirty = false;
+    }
+    if (ws.ctr_dirty) {
+        HIP_TRY(hipMemsetAsync(ws.d_ctr.p, 0, 256, st));
+        ws.ctr_dirty = false;
+    }
     return 0;
 }
 
-bool lean_pipe() {  // RC_PIPE_LEAN=0: the round-3 first version's extra event packets
-    const char *e = getenv("RC_PIPE_LEAN");
-    return !(e && e[0] == '0');
+// A launch sequence that failed after its tile kernel was queued: wait for whatever it queued
+// (this workspace's buffers are reused by the call after next) and leave the grab counter to be
+// re-zeroed -- its edge kernel, which zeroes it, may never have been queued.  Returns `rc`.
+int abandon_launch(Workspace &ws, hipStream_t ts, hipStream_t xs, int rc) {
+    (void)hipStreamSynchronize(ts);
+    if (xs != ts) (void)hipStreamSynchronize(xs);
+    ws.ctr_dirty = true;
+    ws.pending = false;
+    return rc;
 }
 
 // batches of at least this many streams walk their chains one lane per stream (when the
@@ -431,7 +496,6 @@ int upload_and_launch(rc_chunker *ch, Workspace &ws, const Plan &plan, ChainPara
     // counts, merge points, slice offsets, slices and repaired counts of the parallel join
     // (kernels.hip)
     if (int rc = ws.d_seg_counts.ensure(std::max<uint64_t>(plan.n_segs, 1) * 40)) return rc;
-    if (int rc = ensure_ctr(ws)) return rc;
     // The upload goes on the copy stream: stage_descriptors already waited for the call that
     // last used this workspace, so its device buffer is free now, while the previous call's
     // kernels may still be running on `stream`.  `stream` waits for the upload only.
@@ -449,10 +513,8 @@ int upload_and_launch(rc_chunker *ch, Workspace &ws, const Plan &plan, ChainPara
         // RC_PIPELINE_END: nothing follows for this chain to overlap, so it runs on every CU
         xs = end ? ch->fstream : ch->xstream;
         // the inputs: nothing to wait for when the caller's stream has no work pending (each
-        // event record and wait is a packet between two tile kernels; RC_PIPE_LEAN=0 keeps them)
-        const char *lean = getenv("RC_PIPE_LEAN");
-        const bool lean_on = !(lean && lean[0] == '0');
-        if (!lean_on || hipStreamQuery(stream) != hipSuccess) {
+        // event record and wait is a packet between two tile kernels)
+        if (hipStreamQuery(stream) != hipSuccess) {
             HIP_TRY(hipEventRecord(ch->in_ev[wi], stream));
             HIP_TRY(hipStreamWaitEvent(ts, ch->in_ev[wi], 0));
         }
@@ -461,6 +523,7 @@ int upload_and_launch(rc_chunker *ch, Workspace &ws, const Plan &plan, ChainPara
         HIP_TRY(hipStreamWaitEvent(xs, ch->ws[wi ^ 1].done, 0));
     }
     HIP_TRY(hipStreamWaitEvent(ts, ch->uploaded[wi], 0));
+    if (int rc = ensure_ctr(ws, ts)) return rc;
     const StreamDesc d = desc_view(ws.d_desc.p, plan.n);
     std::array<hipEvent_t, 4> ev{};
     if (ch->timing) {
@@ -478,14 +541,12 @@ int upload_and_launch(rc_chunker *ch, Workspace &ws, const Plan &plan, ChainPara
     prm.grp = grp;
     prm.n_tiles = plan.n_tiles;
     // lane-per-stream chain (kernels.hip rc_lane_chain_kernel) for batches of many streams;
-    // RC_LANE_CHAIN=0 never, =1 whatever the count, =lane one lane per stream instead of a quad
-    // (read per call: tests switch it)
-    {
-        const char *e = getenv("RC_LANE_CHAIN");
-        prm.lane = e && e[0] == '0'   ? 0u
-                   : e && e[0] == '1' ? 2u
-                   : e && e[0] == 'l' ? 3u  // "lane": one lane per stream instead of a quad
-                   : plan.n >= kLaneMinStreams ? 1u : 0u;
+    // RC_LANE_CHAIN: auto, 0 never, 1 whatever the count, lane one lane per stream (not a quad)
+    switch (ch->knobs[knLaneChain]) {
+    case 1: prm.lane = 0u; break;
+    case 2: prm.lane = 2u; break;
+    case 3: prm.lane = 3u; break;
+    default: prm.lane = plan.n >= kLaneMinStreams ? 1u : 0u;
     }
     // 32-bit chain steps: small windows (the one-row record cache) and key indices < 2^32
     prm.lean = ch->small && plan.max_len < (16ull << 30) ? 1u : 0u;
@@ -495,16 +556,27 @@ int upload_and_launch(rc_chunker *ch, Workspace &ws, const Plan &plan, ChainPara
                         static_cast<uint32_t *>(ws.d_ctr.p), ts, ch->timing ? ev[1] : nullptr,
                         pipelined ? ch->tile_cus : 0u, xs,
                         // the timing event after the tile kernel doubles as the hand-over event
-                        !pipelined ? nullptr : ch->timing && lean_pipe() ? ev[1] : ch->tiled[wi]))
-        return fail(RC_ERR_HIP, "%s", rc_launch_error());
-    if (ch->timing) HIP_TRY(hipEventRecord(ev[2], xs));
+                        !pipelined ? nullptr : ch->timing ? ev[1] : ch->tiled[wi], ch->sched))
+        return abandon_launch(ws, ts, xs, fail(RC_ERR_HIP, "%s", rc_launch_error()));
+    // A call in sequence after a pipelined one: that call's chain runs on another stream and
+    // may still be writing cuts and counts that this call's chain writes too (calls may share
+    // output arrays), so this chain waits for it.  (Pipelined calls wait above.)
+    const Workspace &prev = ch->ws[wi ^ 1];
+    if (!pipelined && prev.piped && hipStreamWaitEvent(xs, prev.done, 0) != hipSuccess)
+        return abandon_launch(ws, ts, xs, fail(RC_ERR_HIP, "hipStreamWaitEvent failed"));
+    if (ch->timing && hipEventRecord(ev[2], xs) != hipSuccess)
+        return abandon_launch(ws, ts, xs, fail(RC_ERR_HIP, "hipEventRecord failed"));
+    const uint32_t join = (ch->knobs[knJoinWalk] ? RC_JOIN_WALK_ONLY : 0u) |
+                          (ch->knobs[knRepair] ? RC_JOIN_REPAIR : 0u);
     if (rc_launch_chain(ch->d_tables, d, plan.n, prm, plan.n_segs,
                         static_cast<const TileRecord *>(ws.d_records.p), d_cuts, d_counts,
                         static_cast<uint64_t *>(ws.d_scratch.p),
-                        static_cast<uint64_t *>(ws.d_seg_counts.p), plan.any_multi, xs))
-        return fail(RC_ERR_HIP, "%s", rc_launch_error());
-    HIP_TRY(hipEventRecord(ws.done, xs));
+                        static_cast<uint64_t *>(ws.d_seg_counts.p), plan.any_multi, join, xs))
+        return abandon_launch(ws, ts, xs, fail(RC_ERR_HIP, "%s", rc_launch_error()));
+    if (hipEventRecord(ws.done, xs) != hipSuccess)
+        return abandon_launch(ws, ts, xs, fail(RC_ERR_HIP, "hipEventRecord failed"));
     ws.pending = true;
+    ws.piped = pipelined;
     if (ch->timing) {
         HIP_TRY(hipEventRecord(ev[3], xs));
         ch->ev_rec.push_back(ev);
@@ -512,25 +584,19 @@ int upload_and_launch(rc_chunker *ch, Workspace &ws, const Plan &plan, ChainPara
     return 0;
 }
 
-// CUs reserved for the edge and chain kernels of pipelined calls when rc_chunker_overlap /
-// RC_OVERLAP_CUS do not say: one per shader engine (4 per XCD).  Measured on one allocation
+// CUs reserved for the edge and chain kernels of pipelined calls when rc_chunker_overlap does
+// not say (RC_OVERLAP_CUS, knobs.h, default 32): one per shader engine (4 per XCD).  Measured on one allocation
 // (scripts/overlap_ab.py, profiles/r03/overlap/): reserving 8 or 16 CUs left the shader
 // engines of an XCD unequal and the persistent tile kernel 15 % slower (config 2: 11.3 and
 // 11.7 ms against 9.87 unpipelined -- a workgroup the dispatcher sends to a full engine waits
 // for the end of the launch); 32 keeps every engine at 7 CUs and the tile kernel at 9.84 ms.
-constexpr uint32_t kDefaultReserve = 32;
-
 // The two streams of overlap mode.  KFD spreads the bits of a queue's CU mask over the XCDs
 // first (bit i -> XCD i % 8), then over that XCD's shader engines (bits 0-7 engine 0, 8-15
 // engine 1, ...), so the first `reserve` bits take reserve / 8 CUs of every XCD and, for a
 // multiple of 32, the same number of every engine (scripts/ubench/cumask_probe.hip reads the
 // CUs each mask runs on: disjoint, 2 or 4 per XCD).
 int setup_overlap(rc_chunker *ch) {
-    uint32_t want = ch->reserve_req;
-    if (!want) {
-        want = kDefaultReserve;
-        if (const char *e = getenv("RC_OVERLAP_CUS")) want = (uint32_t)strtoul(e, nullptr, 0);
-    }
+    const uint32_t want = ch->reserve_req ? ch->reserve_req : (uint32_t)ch->knobs[knOverlapCus];
     if (ch->tstream && ch->reserve == want) return 0;
     int cus = 0;
     HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ch->device));
@@ -630,6 +696,9 @@ int rc_chunker_create(uint64_t min_length, uint64_t max_length, const uint8_t *k
         return fail(RC_ERR_MIN_GT_MAX, "Minimum length is greater than the maximum one");
     const uint64_t k0 = load_le64(key), k1 = load_le64(key + 8);
     if (k0 == 0) return fail(RC_ERR_BAD_KEY, "Bad key contents");
+    // the environment knobs (knobs.h), once: a malformed one is an error, not a silent default
+    Knobs knobs;
+    if (read_knobs(knobs, g_err, sizeof g_err)) return RC_ERR_ARGUMENT;
 
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
@@ -646,33 +715,30 @@ int rc_chunker_create(uint64_t min_length, uint64_t max_length, const uint8_t *k
     ch->window = window_keys(max_length);
     // a window (plus its two edge tiles) within one 64-tile row of the chain's record cache:
     // the chain's edge ranges are then a large part of its work, and group maxima trim them
+    ch->knobs = knobs;
     ch->small = ch->window / kTileKeys + 3 <= 64;
-    ch->groups = ch->small;
-    if (const char *e = getenv("RC_TILE_GROUPS_OFF")) ch->groups = ch->groups && e[0] != '1';
-    // RC_TILE_GROUPS_ON=1: group records for large windows too (the chains trim their edge
-    // ranges with them, chain_step); measured before it becomes a default
-    if (const char *e = getenv("RC_TILE_GROUPS_ON")) ch->groups = ch->groups || e[0] == '1';
-    if (const char *e = getenv("RC_CHAIN_LEAN_OFF")) ch->small = ch->small && e[0] != '1';
+    // RC_TILE_GROUPS=1: group records for large windows too (the chains trim their edge ranges
+    // with them, chain_step; measured slower); =0: never
+    ch->groups = knobs[knTileGroups] == 0 ? ch->small : knobs[knTileGroups] == 2;
+    if (knobs[knChainLean] == 1) ch->small = false;  // RC_CHAIN_LEAN=0
+    ch->sched.permille = (uint32_t)knobs[knTileStatic];
+    ch->sched.chunk = (uint32_t)knobs[knTileChunk];
+    ch->sched.dyn_min = (uint32_t)knobs[knTileDynMin];
     ch->k0 = k0;
     ch->k1 = k1;
     ch->device = device;
     build_tables(k0, k1, ch->tables);
-    {
-        // chain segmentation knobs (RC_SEGMENT_BYTES forces a segment length; RC_SEGMENT_EXT
-        // sets the speculative extension); the per-call choice is made in stage_descriptors
-        if (const char *e = getenv("RC_SEGMENT_BYTES")) ch->seg_force = strtoull(e, nullptr, 0);
-        // 2 steps past the segment end, segments of at least 2 x max (round 3, with boundary
-        // repair in the merge kernel: a boundary whose chains miss is continued where it is,
-        // where before one miss sent the whole stream to the sequential join, so round 2 ran 4
-        // steps over 3 x max).  One allocation each (scripts/chain_ab.py, profiles/r03/repair/):
-        // the harness's chain 0.108 -> 0.091 ms, 3 (ii) 0.241 -> 0.231, config 4 0.268 ->
-        // 0.253, config 2 0.159 -> 0.152; 1 x max segments with 1 step miss past the next
-        // list and fall back (1.76 ms on the harness)
-        ch->ext_steps = 2;
-        if (const char *e = getenv("RC_SEGMENT_EXT")) ch->ext_steps = strtoull(e, nullptr, 0);
-        // RC_SEGMENT_FLOOR: the shortest segment in max_lengths (measurements)
-        if (const char *e = getenv("RC_SEGMENT_FLOOR")) ch->seg_floor = std::max<uint64_t>(strtoull(e, nullptr, 0), 1);
-    }
+    // chain segmentation (RC_SEGMENT_BYTES forces a segment length; the per-call choice is made
+    // in stage_descriptors).  2 extension steps past the segment end, segments of at least 2 x
+    // max (round 3, with boundary repair in the merge kernel: a boundary whose chains miss is
+    // continued where it is, where before one miss sent the whole stream to the sequential join,
+    // so round 2 ran 4 steps over 3 x max).  One allocation each (scripts/chain_ab.py,
+    // profiles/r03/repair/): the harness's chain 0.108 -> 0.091 ms, 3 (ii) 0.241 -> 0.231, config
+    // 4 0.268 -> 0.253, config 2 0.159 -> 0.152; 1 x max segments with 1 step miss past the next
+    // list and fall back (1.76 ms on the harness)
+    ch->seg_force = (uint64_t)knobs[knSegmentBytes];
+    ch->ext_steps = (uint64_t)knobs[knSegmentExt];
+    ch->seg_floor = (uint64_t)knobs[knSegmentFloor];
     {
         DeviceGuard g(device);
         hipError_t e = hipMalloc(&ch->d_tables, sizeof(KeyTables));
@@ -685,12 +751,14 @@ int rc_chunker_create(uint64_t min_length, uint64_t max_length, const uint8_t *k
             return fail(RC_ERR_HIP, "device setup failed: %s", hipGetErrorString(e));
         }
     }
+    rc_track(ch, [](void *h) { rc_chunker_destroy(static_cast<rc_chunker *>(h)); });
     *out = ch;
     return RC_OK;
 }
 
 void rc_chunker_destroy(rc_chunker *ch) {
     if (!ch) return;
+    rc_untrack(ch);
     {
         DeviceGuard g(ch->device);
         (void)hipDeviceSynchronize();
@@ -835,8 +903,9 @@ int rc_chunk_device(rc_chunker *ch, uint64_t n, const uint8_t *const *d_streams,
     // * launches on the tile kernel's static schedule (fewer than 128 tiles per wave: the
     //   harness's one 5.12 GB stream): on 224 CUs the static shares grow, 0.85 -> 0.92 ms.
     // RC_PIPE_ALL=1 pipelines every call (tests, measurements).
-    const char *pa = getenv("RC_PIPE_ALL");
-    const bool all = pa && pa[0] == '1';
+    std::lock_guard<std::mutex> lock(ch->mu);
+    DeviceGuard g(ch->device);  // rc_tile_dynamic counts the CUs of the current device
+    const bool all = ch->knobs[knPipeAll] != 0;
     bool pipelined = (flags & RC_PIPELINED) != 0 && (all || !ch->groups);
     if (pipelined && !all) {
         uint64_t tiles = 0;
@@ -845,11 +914,9 @@ int rc_chunk_device(rc_chunker *ch, uint64_t n, const uint8_t *const *d_streams,
             const uint64_t jn = rc_keys_needed(ch->max_length, lens[i], P);
             tiles += jn ? jn / kTileKeys + 1 : 0;
         }
-        pipelined = rc_tile_dynamic(tiles, 0) != 0;
+        pipelined = rc_tile_dynamic(tiles, 0, ch->sched) != 0;
     }
 
-    std::lock_guard<std::mutex> lock(ch->mu);
-    DeviceGuard g(ch->device);
     // no CU-masked streams on this device / runtime: the request runs in sequence (the call
     // stays correct; rc_chunker_overlap reports the error, rc_chunker_overlap_cus stays 0)
     if (pipelined && !ch->overlap_failed && setup_overlap(ch) != 0) {
@@ -1028,14 +1095,15 @@ int rc_tile_records(rc_chunker *ch, uint64_t n, const uint8_t *const *d_streams,
     if (int rc = stage_descriptors(ch, ws, n, d_streams, lens, last_piece, plan)) return rc;
     if (int rc = ws.d_desc.ensure(plan.bytes)) return rc;
     if (int rc = ws.d_records.ensure(records_bytes(plan))) return rc;
-    if (int rc = ensure_ctr(ws)) return rc;
     HIP_TRY(hipMemcpy(ws.d_desc.p, ws.h_desc.p, plan.bytes, hipMemcpyHostToDevice));
+    if (int rc = ensure_ctr(ws, nullptr)) return rc;
     GroupRecord *d_grp = ch->groups ? group_records(ws, plan) : nullptr;
     if (rc_launch_tiles(ch->d_tables, desc_view(ws.d_desc.p, n), n, plan.n_tiles,
                         static_cast<TileRecord *>(ws.d_records.p), d_grp,
                         group_hot_threshold(ch->window), tie_lists(ws, plan),
-                        static_cast<uint32_t *>(ws.d_ctr.p), nullptr, nullptr, 0u, nullptr, nullptr))
-        return fail(RC_ERR_HIP, "%s", rc_launch_error());
+                        static_cast<uint32_t *>(ws.d_ctr.p), nullptr, nullptr, 0u, nullptr, nullptr,
+                        ch->sched))
+        return abandon_launch(ws, nullptr, nullptr, fail(RC_ERR_HIP, "%s", rc_launch_error()));
     HIP_TRY(hipDeviceSynchronize());
     std::vector<TileRecord> h(plan.n_tiles);
     std::vector<GroupRecord> hg(plan.n_tiles, GroupRecord{~0ull, {~0ull, ~0ull, ~0ull, ~0ull}, 0ull});
@@ -1096,7 +1164,8 @@ int rc_timing_read(rc_chunker *ch, double *phase_a_ms, double *phase_b_ms, uint6
 int rc_read_probe(const uint8_t *d_src, uint64_t nbytes, uint32_t *d_out, void *hip_stream) {
     if (nbytes && (!d_src || !d_out)) return fail(RC_ERR_ARGUMENT, "null argument");
     if (reinterpret_cast<uintptr_t>(d_src) & 15) return fail(RC_ERR_ALIGN, "source not 16-byte aligned");
-    if (rc_launch_read_probe(d_src, nbytes, d_out, hip_stream)) return fail(RC_ERR_HIP, "%s", rc_launch_error());
+    if (rc_launch_read_probe(d_src, nbytes, d_out, (uint32_t)process_knobs()[knProbeBlock], hip_stream))
+        return fail(RC_ERR_HIP, "%s", rc_launch_error());
     return RC_OK;
 }
 

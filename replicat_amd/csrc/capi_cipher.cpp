@@ -17,6 +17,7 @@
 
 #include "../../include/replicat_cipher.h"
 #include "capi_internal.h"
+#include "knobs.h"
 #include "cipher_kernels.h"
 #include "digest_kernels.h"
 
@@ -24,11 +25,8 @@ static_assert(sizeof(GcmItem) == 48, "GcmItem is a 48-byte device record");
 
 namespace {
 
-// RC_GCM_DEBUG=1: every host step of a call is stamped on stderr (hang diagnosis)
-bool debug_on() {
-    static const bool on = std::getenv("RC_GCM_DEBUG") != nullptr;
-    return on;
-}
+// RC_GCM_DEBUG=1 (knobs.h): every host step of a call is stamped on stderr (hang diagnosis)
+bool debug_on() { return rc::process_knobs()[rc::knGcmDebug] != 0; }
 #define GCM_DBG(...)                                      \
     do {                                                  \
         if (debug_on()) {                                 \
@@ -287,6 +285,11 @@ int rc_gcm_create(uint32_t key_bits, uint32_t nonce_bits, int device, rc_gcm **o
     const uint32_t nonce_bytes = nonce_bits / 8;
     if (nonce_bytes < 8 || nonce_bytes > 128)
         return rc_fail(RC_ERR_NONCE_SIZE, "Nonce must be between 8 and 128 bytes");
+    {  // the environment knobs (knobs.h): a malformed one fails every handle's creation
+        rc::Knobs knobs;
+        char err[256];
+        if (rc::read_knobs(knobs, err, sizeof err)) return rc_fail(RC_ERR_ARGUMENT, "%s", err);
+    }
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count)
         return rc_fail(RC_ERR_NO_DEVICE, "no HIP device %d", device);
@@ -313,12 +316,14 @@ int rc_gcm_create(uint32_t key_bits, uint32_t nonce_bits, int device, rc_gcm **o
         rc_gcm_destroy(g);
         return rc;
     }
+    rc_track(g, [](void *p) { rc_gcm_destroy(static_cast<rc_gcm *>(p)); });
     *out = g;
     return RC_OK;
 }
 
 void rc_gcm_destroy(rc_gcm *g) {
     if (!g) return;
+    rc_untrack(g);
     {
         DeviceGuard guard(g->device);
         (void)hipDeviceSynchronize();

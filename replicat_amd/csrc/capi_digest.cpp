@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "capi_internal.h"
+#include "knobs.h"
 #include "digest_kernels.h"
 
 static_assert(sizeof(rc_blake2b_state) == 256, "rc_blake2b_state is a 256-byte device record");
@@ -79,6 +80,7 @@ struct Guard {
 struct rc_hasher {
     uint32_t digest_size = 64;
     int device = 0;
+    rc::Knobs knobs;  // knobs.h, read once at creation (the lane / quad split)
     std::mutex mu;
     struct Workspace {
         PinnedMem h_stage;   // host-built descriptors / items
@@ -155,9 +157,10 @@ int enqueue_items(rc_hasher *h, uint64_t n, const uint8_t *const *d_ptrs, const 
     if (int rc = timing_begin(h, st, ev)) return rc;
     uint64_t msg_bytes = 0;
     for (uint64_t i = 0; i < n; ++i) msg_bytes += lens[i];
-    const uint64_t lane_max = rc_b2_lane_max(msg_bytes, it[0].len);
+    const uint64_t lane_max = rc_b2_lane_max(msg_bytes, it[0].len, h->knobs[rc::knB2LaneMax]);
     if (rc_b2_launch_items(static_cast<const B2Item *>(w->d_stage.p), n, h->digest_size, d_out,
-                           lane_max, rc_b2_lane_only(lane_max, it[0].len), st))
+                           lane_max, rc_b2_lane_only(lane_max, it[0].len, h->knobs[rc::knB2LaneOnly]),
+                           st))
         return rc_fail(RC_ERR_HIP, "%s", rc_b2_launch_error());
     if (int rc = timing_end(h, st, ev)) return rc;
     return finish(h, *w, st);
@@ -222,13 +225,18 @@ int rc_hasher_enqueue_chunks(rc_hasher *h, uint64_t n, const uint8_t *const *d_p
     std::array<hipEvent_t, 2> ev{};
     if (int rc = timing_begin(h, st, ev)) return rc;
     uint32_t *hist = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(w->d_stage.p) + hist_off);
-    const uint64_t lane_max = rc_b2_lane_max(bytes, longest);
+    const uint64_t lane_max = rc_b2_lane_max(bytes, longest, h->knobs[rc::knB2LaneMax]);
     if (rc_b2_launch_chunks(n, d, d + n, d_cuts, d_counts, chunk_off, hist,
                             static_cast<B2Item *>(w->d_items.p), total_cap, h->digest_size, d_out,
-                            lane_max, rc_b2_lane_only(lane_max, longest), st))
+                            lane_max, rc_b2_lane_only(lane_max, longest, h->knobs[rc::knB2LaneOnly]),
+                            st))
         return rc_fail(RC_ERR_HIP, "%s", rc_b2_launch_error());
     if (int rc = timing_end(h, st, ev)) return rc;
     return finish(h, *w, st);
+}
+
+namespace {
+thread_local char g_knob_err[256];
 }
 
 extern "C" {
@@ -238,11 +246,15 @@ int rc_blake2b_create(uint32_t digest_size, int device, rc_hasher **out) {
     *out = nullptr;
     if (digest_size < 1 || digest_size > 64)
         return rc_fail(RC_ERR_DIGEST_SIZE, "digest_size must be between 1 and 64 bytes");
+    rc::Knobs knobs;
+    if (rc::read_knobs(knobs, g_knob_err, sizeof g_knob_err))
+        return rc_fail(RC_ERR_ARGUMENT, "%s", g_knob_err);
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count)
         return rc_fail(RC_ERR_NO_DEVICE, "no HIP device %d", device);
     Guard g(device);
     rc_hasher *h = new rc_hasher;
+    h->knobs = knobs;
     h->digest_size = digest_size;
     h->device = device;
     for (auto &w : h->ws) {
@@ -252,12 +264,14 @@ int rc_blake2b_create(uint32_t digest_size, int device, rc_hasher **out) {
             return rc_fail(RC_ERR_HIP, "hipEventCreate failed: %s", hipGetErrorString(e));
         }
     }
+    rc_track(h, [](void *p) { rc_blake2b_destroy(static_cast<rc_hasher *>(p)); });
     *out = h;
     return RC_OK;
 }
 
 void rc_blake2b_destroy(rc_hasher *h) {
     if (!h) return;
+    rc_untrack(h);
     {
         Guard g(h->device);
         (void)hipDeviceSynchronize();

@@ -8,6 +8,15 @@
 // Sets the calling thread's rc_last_error() message and returns `code`.
 int rc_fail(int code, const char *fmt, ...);
 
+// Live handles (chunkers, hashers, ciphers): every *_create registers its handle with the
+// destroy function that releases it, every *_destroy unregisters it.  The first registration
+// installs an atexit hook that destroys whatever is still registered when the process exits --
+// after the caller's own teardown (Python's finalisation included) and BEFORE the HIP runtime's
+// static destructors, which ran later than a leaked CU-masked stream's teardown can (round 3:
+// a process that exited with a pipelined chunker alive died in __cxa_finalize).
+void rc_track(void *handle, void (*destroy)(void *));
+void rc_untrack(void *handle);
+
 #define RC_HIP_TRY(expr)                                                                 \
     do {                                                                                 \
         const hipError_t e_ = (expr);                                                    \

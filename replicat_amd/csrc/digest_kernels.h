@@ -58,16 +58,16 @@ int rc_b2_launch_chunks(uint64_t n, const uint64_t *d_ptrs, const uint64_t *d_cu
 // bytes >= longest << 16; otherwise every item goes to quads (config 2: its 5 MB chunks' chains
 // set the time, and lanes sharing their SIMDs only lengthen them).  Within a throughput-bound
 // batch a message goes to a lane when its chain (~3x a quad's) ends well inside the batch time:
-// len <= bytes >> 17.  RC_B2_LANE_MAX (bytes) overrides the whole rule, 0 turning lanes off.
-inline uint64_t rc_b2_lane_max(uint64_t bytes, uint64_t longest) {
-    if (const char *e = getenv("RC_B2_LANE_MAX")) return strtoull(e, nullptr, 0);
+// len <= bytes >> 17.  knob_max (RC_B2_LANE_MAX, knobs.h: -1 = the rule) overrides the whole
+// rule, 0 turning lanes off.
+inline uint64_t rc_b2_lane_max(uint64_t bytes, uint64_t longest, int64_t knob_max) {
+    if (knob_max >= 0) return (uint64_t)knob_max;
     return longest > (bytes >> 16) ? 0 : bytes >> 17;
 }
 // Whether a batch whose messages are at most `longest` bytes goes to the lane kernel alone
-// (RC_B2_LANE_ONLY=0: never -- the fused kernel's lane role instead, for A/B runs).
-inline bool rc_b2_lane_only(uint64_t lane_max, uint64_t longest) {
-    if (const char *e = getenv("RC_B2_LANE_ONLY"))
-        if (e[0] == '0') return false;
+// (never_only, RC_B2_LANE_ONLY=0: the fused kernel's lane role instead, for A/B runs).
+inline bool rc_b2_lane_only(uint64_t lane_max, uint64_t longest, bool never_only) {
+    if (never_only) return false;
     return lane_max != 0 && longest <= lane_max;
 }
 

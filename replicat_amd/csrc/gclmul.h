@@ -110,6 +110,15 @@ struct ChainParams {
     uint32_t hot;         // the group records' hot threshold (group_hot_threshold)
 };
 
+// The tile kernel's work schedule (kernels.hip tile_units; knobs.h RC_TILE_STATIC / CHUNK /
+// DYN_MIN): the share of the tiles handed out statically (per mille), the dynamic unit size and
+// the tiles per wave from which a launch hands out dynamic units at all.
+struct TileSched {
+    uint32_t permille = 100;
+    uint32_t chunk = 12;
+    uint32_t dyn_min = 128;
+};
+
 // splitmix64 finaliser (replicat_amd/synth.py)
 __host__ __device__ inline uint64_t splitmix64(uint64_t x) {
     uint64_t z = x + 0x9E3779B97F4A7C15ull;
@@ -132,22 +141,28 @@ extern "C" {
 // cus: the CUs the tile kernel's stream may use (its persistent grid; 0 = every CU of the
 // device).  edge_stream (may be NULL = stream): where the edge kernel runs; when it differs,
 // `tiled` (a hipEvent_t) is recorded after the tile kernel and edge_stream waits for it.
+// sched: the chunker's schedule knobs.
 int rc_launch_tiles(const rc::KeyTables *d_tables, rc::StreamDesc desc, uint64_t n_streams,
                     uint64_t n_tiles, rc::TileRecord *d_records, rc::GroupRecord *d_grp,
                     uint32_t hot, uint32_t *d_xlist, uint32_t *d_ctr, void *stream,
-                    void *mid_event, uint32_t cus, void *edge_stream, void *tiled);
+                    void *mid_event, uint32_t cus, void *edge_stream, void *tiled,
+                    rc::TileSched sched);
 uint64_t rc_tie_list_words(uint64_t n_tiles);
-// 1 if a tile launch over n_tiles on `cus` CUs (0 = all) hands out dynamic units, 0 if it is
-// fully static (fewer than kDynMinPerWave tiles per wave)
-int rc_tile_dynamic(uint64_t n_tiles, uint32_t cus);
+// 1 if a tile launch over n_tiles on `cus` CUs of the CURRENT device (0 = all) hands out dynamic
+// units, 0 if it is fully static (fewer than sched.dyn_min tiles per wave)
+int rc_tile_dynamic(uint64_t n_tiles, uint32_t cus, rc::TileSched sched);
+// join: RC_JOIN_* bits -- how multi-segment streams are spliced
+enum : uint32_t { RC_JOIN_WALK_ONLY = 1, RC_JOIN_REPAIR = 2 };
 int rc_launch_chain(const rc::KeyTables *d_tables, rc::StreamDesc desc, uint64_t n_streams,
                     rc::ChainParams prm, uint64_t n_segs, const rc::TileRecord *d_records,
                     uint64_t *d_cuts, int64_t *d_counts, uint64_t *d_scratch,
-                    uint64_t *d_seg_counts, bool any_multi, void *stream);
+                    uint64_t *d_seg_counts, bool any_multi, uint32_t join, void *stream);
 int rc_launch_fill(uint8_t *d_dst, uint64_t nbytes, uint64_t seed, uint64_t stream_id,
                    uint64_t word0, void *stream);
 int rc_launch_fill_streams(uint8_t *d_dst, uint64_t n, uint64_t nbytes, uint64_t slot,
                            uint64_t seed, uint64_t id0, uint64_t id_step, void *stream);
-int rc_launch_read_probe(const uint8_t *d_src, uint64_t nbytes, uint32_t *d_out, void *stream);
+// block: 0 = the tile kernel's default schedule, else interleaved static runs of `block` tiles
+int rc_launch_read_probe(const uint8_t *d_src, uint64_t nbytes, uint32_t *d_out, uint32_t block,
+                         void *stream);
 const char *rc_launch_error(void);
 }

@@ -30,6 +30,7 @@
 #include <stdint.h>
 
 #include "gclmul.h"
+#include "diag.h"
 
 using namespace rc;
 
@@ -44,13 +45,7 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) const u32x4 gu32x4;
 typedef __attribute__((address_space(1))) const uint32_t gu32;
 
-#ifdef RC_PLAIN_LOADS  // diagnostic build: default cache policy for the streamed bytes
-#define RC_STREAM_LOAD(p) (*(p))
-constexpr int kStreamAux = 0;
-#else
-#define RC_STREAM_LOAD(p) __builtin_nontemporal_load(p)
-constexpr int kStreamAux = 2;  // nt
-#endif
+constexpr int kStreamAux = RC_DIAG_STREAM_AUX;  // the streamed bytes' cache policy (nt)
 
 // The tile ring reads through a buffer resource based at the tile: the lane offset stays in one
 // VGPR for the whole kernel and the slot offset is an SGPR, so a reissue costs no address VALU
@@ -337,14 +332,10 @@ __device__ __forceinline__ void tile_scan(const TileRef &tr, const TileRef &nx,
         pf_addrs(x[it].z, lb_a, lb_b, a + 8);
         pf_addrs(x[it].w, lb_a, lb_b, a + 12);
         x[it] = ring_load(nsrc, lane * 16, it);
-#ifdef RC_DIAG_NO_LOOKUPS  // diagnostic build: no table reads (cost split)
-        const uint32_t e0 = a[0] ^ a[1], e1 = a[4] ^ a[5], e2 = a[8] ^ a[9], e3 = a[12] ^ a[13];
-#else
         const uint32_t e0 = pf_gather(a + 0);
         const uint32_t e1 = pf_gather(a + 4);
         const uint32_t e2 = pf_gather(a + 8);
         const uint32_t e3 = pf_gather(a + 12);
-#endif
         // previous word's entry for key 0 of this lane: lane-1's e3 (wave_ror:1); lane 0 takes
         // the carry = lane 63's e3 of the previous iteration (or the word before the tile).
         const uint32_t rot = __builtin_amdgcn_mov_dpp(e3, 0x13C, 0xf, 0xf, false);
@@ -511,18 +502,12 @@ __device__ __forceinline__ GroupRecord tile_groups(const uint32_t (&gpk)[(G + 1)
     return r;
 }
 
-#ifdef RC_DIAG_TILE_STAMPS
-// diagnostic build only: per wave of the tile kernel, s_memrealtime (100 MHz) when its first tile
-// starts and when its last record is stored, and its tile count (scripts/tile_stamps.py)
-__device__ uint64_t g_tile_stamp[3 * 8192];
-#endif
-
 // The tile kernel's work units (round 3): wave w first takes the static unit w, tiles
 // [w s0, (w + 1) s0); the rest of the tiles, from dyn0 = nw s0 on, are dynamic units of `chunk`
 // tiles that waves grab from a counter (one atomic per unit) when they run out of work.  Round 2
 // gave every wave the same static share and measured (RC_DIAG_TILE_STAMPS) the waves of one
 // launch ending between 52 % and 100 % of its time: the slowest waves' tail was ~23 % of the
-// kernel.  Small launches (fewer than kDynMinPerWave tiles per wave) stay fully static.
+// kernel.  Small launches (fewer than TileSched::dyn_min tiles per wave) stay fully static.
 // Static share 25 % and 32-tile units: 10-11 % faster on configs 2, 3 (iii) and 4 than fully
 // static on the same allocation; late in round 3, 10 % and 12-tile units took ~4 % more off
 // (tile_units).
@@ -541,8 +526,9 @@ struct TileUnits {  // tile indices fit 32 bits (the tie lists store them as u32
     }
 };
 
-// Units of a launch over n_tiles tiles by nw waves.  RC_TILE_STATIC (per mille, default 100): the
-// share of the tiles handed out statically; RC_TILE_CHUNK (default 12): dynamic unit size.  Both
+// Units of a launch over n_tiles tiles by nw waves (sched: knobs.h RC_TILE_STATIC, per mille,
+// default 100: the share of the tiles handed out statically; RC_TILE_CHUNK, default 12: dynamic
+// unit size; RC_TILE_DYN_MIN, default 128: fewer tiles per wave stay fully static).  Both
 // measured on one allocation per config (scripts/tile_sched_ab.py, profiles/r03/sched): tile
 // kernel vs the round-2 fully static schedule, config 2 11.06 -> 9.88 ms, 3 (iii) 11.46 -> 10.32,
 // config 4 23.87 -> 21.23; the harness (76 tiles per wave) is fastest fully static.  Units were
@@ -553,17 +539,12 @@ struct TileUnits {  // tile indices fit 32 bits (the tie lists store them as u32
 // launch saturate it.  12 keeps half that rate (3 ii 10.65 -> 10.41 ms, 3 iii and config 4 ~1 %).
 // With 12-tile units a 10 % static share beat 25 % (config 2 9.77 -> 9.68 ms pipelined, 9.78 ->
 // 9.68 sequential, 3 iii 9.98 -> 9.94; 0 %: 9.72; profiles/r03/sched_static/): ~290 k grabs.
-constexpr uint64_t kDynMinPerWave = 128;  // fewer tiles per wave: one static unit each
 constexpr uint64_t kDynChunkMin = 2;    // units of at least 2 tiles
-__host__ inline TileUnits tile_units(uint64_t n_tiles, uint64_t nw) {
+__host__ inline TileUnits tile_units(uint64_t n_tiles, uint64_t nw, TileSched sched) {
     TileUnits U;
     U.n_tiles = (uint32_t)n_tiles;
     U.nw = (uint32_t)nw;
-    uint64_t permille = 100, chunk = 12, dyn_min = kDynMinPerWave;
-    if (const char *e = getenv("RC_TILE_STATIC")) permille = strtoull(e, nullptr, 0);
-    if (const char *e = getenv("RC_TILE_CHUNK")) chunk = strtoull(e, nullptr, 0);
-    // RC_TILE_DYN_MIN (tests): the tiles per wave from which units are dynamic
-    if (const char *e = getenv("RC_TILE_DYN_MIN")) dyn_min = strtoull(e, nullptr, 0);
+    uint64_t permille = sched.permille, chunk = sched.chunk, dyn_min = sched.dyn_min;
     if (permille > 1000) permille = 1000;
     if (chunk < kDynChunkMin) chunk = kDynChunkMin;
     if (n_tiles < dyn_min * nw || permille == 1000) {  // fully static
@@ -622,10 +603,7 @@ __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restri
     uint32_t u = (uint32_t)gw, ub, ue;
     U.range(u, ub, ue);
     uint32_t n_ties = 0;
-#ifdef RC_DIAG_TILE_STAMPS
-    const uint64_t stamp0 = __builtin_amdgcn_s_memrealtime();
-    uint64_t n_done = 0;
-#endif
+    RC_TILE_STAMP_BEGIN();
 
     // the first fast tile, possibly in a later unit (units without one list no ties)
     TileCursor<G == 1> cursor;
@@ -703,13 +681,8 @@ __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restri
         }
 
         // retire the pending tile: (first maximal exact key, index) over its candidate lanes
-#ifndef RC_DIAG_NO_TAIL
         {
-#if defined(RC_DIAG_NO_EXACT)  // diagnostic build: no exact key (cost split; wrong records)
-            const uint64_t k = ((uint64_t)pend_hi << 32) | pend_lo;
-#else
             const uint64_t k = full_key(tl, th, pend_lo, pend_hi);
-#endif
             // a marker carries what the edge kernel needs: candidate lanes, ~stream
             const bool ptie = pend_st >> 31;
             const uint64_t pm = ptie ? 0 : pend_mask;
@@ -749,12 +722,7 @@ __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restri
         const uint8_t *q = cur.base + 4 * (cur.j0 + pend_jl);
         pend_lo = ld_u32(q - (cur.j0 + pend_jl ? 4 : 0));  // never key 0; no read before the stream
         pend_hi = ld_u32(q);
-#else
-        if (lane == 0 && (top ^ first ^ last) == 0x5a5au) rec[t].key = first ^ last;  // keep the scan alive
-#endif
-#ifdef RC_DIAG_TILE_STAMPS
-        ++n_done;
-#endif
+        RC_TILE_STAMP_TILE();
         if (nu != u) {  // cur was its unit's last fast tile: close the unit's tie list
             if (lane == 0) xcount[u] = n_ties;
             n_ties = 0;
@@ -784,13 +752,7 @@ __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restri
             rec[pend_t].key = bk;
             rec[pend_t].j = bj;
             xcount[u] = n_ties;
-#ifdef RC_DIAG_TILE_STAMPS
-            if (gw < 8192) {
-                g_tile_stamp[3 * gw] = stamp0;
-                g_tile_stamp[3 * gw + 1] = __builtin_amdgcn_s_memrealtime();
-                g_tile_stamp[3 * gw + 2] = n_done;
-            }
-#endif
+            RC_TILE_STAMP_END(gw);
         }
     }
 }
@@ -935,9 +897,7 @@ __global__ __launch_bounds__(256) void rc_edge_kernel(const KeyTables *__restric
 struct ChainStream {
     const uint8_t *base;
     uint64_t L, P, tb0, nt, jmax;
-#ifdef RC_DIAG_STAMPS
-    bool diag;
-#endif
+    RC_DIAG_ONLY(bool diag;)
 };
 
 __device__ __forceinline__ ChainStream chain_stream(const StreamDesc &d, uint64_t s) {
@@ -948,9 +908,7 @@ __device__ __forceinline__ ChainStream chain_stream(const StreamDesc &d, uint64_
     st.tb0 = sload(d.tile_base + s);
     st.nt = sload(d.tile_base + s + 1) - st.tb0;
     st.jmax = st.L >= 8 ? (st.L - 4) / 4 : 0;
-#ifdef RC_DIAG_STAMPS
-    st.diag = s == 0;
-#endif
+    RC_DIAG_ONLY(st.diag = s == 0;)
     return st;
 }
 
@@ -1143,30 +1101,6 @@ struct RecCache {
     }
 };
 
-#ifdef RC_DIAG_STAMPS
-// diagnostic build only: per-step s_memrealtime stamps (100 MHz) of stream 0's walker
-__device__ uint64_t g_diag[4096];
-__device__ uint32_t g_diag_n;
-#define RC_STAMP(tag)                                                                  \
-    do {                                                                               \
-        if (st.diag && lane_id() == 0 && g_diag_n < 4000) {                            \
-            g_diag[g_diag_n++] = ((uint64_t)(tag) << 56) | __builtin_amdgcn_s_memrealtime(); \
-        }                                                                              \
-    } while (0)
-#define RC_LSTAMP(tag)                                                                 \
-    do {                                                                               \
-        if (diag && lane_id() == 0 && g_diag_n < 4000) {                               \
-            g_diag[g_diag_n++] = ((uint64_t)(tag) << 56) | __builtin_amdgcn_s_memrealtime(); \
-        }                                                                              \
-    } while (0)
-#else
-#define RC_STAMP(tag) \
-    do {              \
-    } while (0)
-#define RC_LSTAMP(tag) \
-    do {               \
-    } while (0)
-#endif
 
 // One chain step from chunk start `pos` (< L): an argmax cut (adapters.cpp:59-69), or the tail
 // rule's one or two final cuts (adapters.cpp:48-55), or stop (non-final wait / S7 UB).
@@ -1593,12 +1527,8 @@ __global__ __launch_bounds__(kChainWaves * 64) void rc_spec_kernel(const KeyTabl
     const uint64_t s = find_index(d.seg_base, n_streams + 1, q);
     const uint64_t sb = sload(d.seg_base + s), nseg = sload(d.seg_base + s + 1) - sb;
     const uint64_t i = q - sb;
-#ifdef RC_DIAG_STAMPS
     ChainStream st = chain_stream(d, s);
-    st.diag = st.diag && i == (nseg > 8 ? 7 : 0);  // one walker of stream 0 (a mid segment)
-#else
-    const ChainStream st = chain_stream(d, s);
-#endif
+    RC_DIAG_ONLY(st.diag = st.diag && i == (nseg > 8 ? 7 : 0);)  // one walker of stream 0 (mid)
     const bool direct = nseg == 1;
     uint64_t *out = direct ? cuts + sload(d.cut_base + s) : scratch + sload(d.scratch_base + s) + i * prm.seg_cap;
     const uint64_t cap = direct ? sload(d.cut_cap + s) : prm.seg_cap;
@@ -1859,9 +1789,7 @@ __global__ __launch_bounds__(256) void rc_lane_chain_kernel(const KeyTables *__r
 
     uint64_t pos = 0, n = 0;
     bool walking = mine && L > 0 && prm.max_steps > 0, overflow = false;
-#ifdef RC_DIAG_STAMPS
-    const bool diag = gid < 64;  // wave 0: per-phase stamps (diagnostic build only)
-#endif
+    RC_DIAG_ONLY(const bool diag = gid < 64;)  // wave 0: per-phase stamps
     for (;;) {
         if (!__any(walking)) break;
         RC_LSTAMP(1);
@@ -2155,9 +2083,7 @@ __global__ __launch_bounds__(256) void rc_quad_chain_kernel(const KeyTables *__r
 
     uint64_t pos = 0, n = 0;
     bool walking = mine && L > 0 && prm.max_steps > 0, overflow = false;
-#ifdef RC_DIAG_STAMPS
-    const bool diag = gid < 16 && q == 0;  // wave 0 (diagnostic build only)
-#endif
+    RC_DIAG_ONLY(const bool diag = gid < 16 && q == 0;)  // wave 0
     for (;;) {
         if (!__any(walking)) break;
         RC_LSTAMP(1);
@@ -2860,16 +2786,6 @@ int launch_status(const char *what) {
     return 1;
 }
 
-bool rc_join_walk_only() {  // read per launch: tests switch it within one process
-    const char *e = getenv("RC_JOIN_WALK");
-    return e && e[0] == '1';
-}
-
-bool rc_repair_on() {  // RC_REPAIR=0: no repair (the round-2 fallback: any miss walks the stream)
-    const char *e = getenv("RC_REPAIR");
-    return !(e && e[0] == '0');
-}
-
 int cu_count() {
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 256;
@@ -2885,31 +2801,11 @@ extern "C" {
 
 const char *rc_launch_error(void) { return g_launch_err; }
 
-#ifdef RC_DIAG_TILE_STAMPS
-int rc_diag_tile_read(uint64_t *out, uint32_t waves) {
-    if (waves > 8192) waves = 8192;
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tile_stamp), 3 * 8 * (size_t)waves) != hipSuccess) return 1;
-    static uint64_t zero[3 * 8192];
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_tile_stamp), zero, sizeof zero) != hipSuccess;
-}
-#endif
-
-#ifdef RC_DIAG_STAMPS
-int rc_diag_read(uint64_t *out, uint32_t cap, uint32_t *n) {
-    uint32_t k = 0;
-    if (hipMemcpyFromSymbol(&k, HIP_SYMBOL(g_diag_n), 4) != hipSuccess) return 1;
-    if (k > cap) k = cap;
-    if (k && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag), k * 8) != hipSuccess) return 1;
-    *n = k;
-    const uint32_t z = 0;
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_diag_n), &z, 4) != hipSuccess;
-}
-#endif
-
 int rc_launch_tiles(const KeyTables *d_tables, StreamDesc desc, uint64_t n_streams,
                     uint64_t n_tiles, TileRecord *d_records, GroupRecord *d_grp,
                     uint32_t hot, uint32_t *d_xlist, uint32_t *d_ctr, void *stream,
-                    void *mid_event, uint32_t tile_cus, void *edge_stream, void *tiled) {
+                    void *mid_event, uint32_t tile_cus, void *edge_stream, void *tiled,
+                    TileSched sched) {
     hipStream_t st = (hipStream_t)stream;
     hipStream_t est = edge_stream ? (hipStream_t)edge_stream : st;
     // the edge kernel's stream follows the tile kernel (also when there are no tiles)
@@ -2932,7 +2828,7 @@ int rc_launch_tiles(const KeyTables *d_tables, StreamDesc desc, uint64_t n_strea
     const uint64_t cus = tile_cus ? (uint64_t)tile_cus : (uint64_t)cu_count();
     if (grid > cus) grid = cus;  // persistent: one 144 KiB-LDS workgroup per CU
     const uint64_t n_waves = grid * waves_per_wg;
-    const TileUnits U = tile_units(n_tiles, n_waves);
+    const TileUnits U = tile_units(n_tiles, n_waves, sched);
     // the tie lists: n_tiles slots, one count per unit; d_ctr is 0 (the edge kernel re-zeros it)
     uint32_t *d_xcount = d_xlist + n_tiles;
     if (d_grp)
@@ -2964,16 +2860,17 @@ uint64_t rc_tie_list_words(uint64_t n_tiles) {
     return 2 * n_tiles + n_tiles / kDynChunkMin + 64;
 }
 
-int rc_tile_dynamic(uint64_t n_tiles, uint32_t cus) {
+int rc_tile_dynamic(uint64_t n_tiles, uint32_t cus, TileSched sched) {
     if (n_tiles == 0) return 0;
-    const TileUnits U = tile_units(n_tiles, (uint64_t)(cus ? cus : (uint32_t)cu_count()) * (1024 / kWaveSize));
+    const TileUnits U = tile_units(n_tiles, (uint64_t)(cus ? cus : (uint32_t)cu_count()) * (1024 / kWaveSize),
+                                   sched);
     return U.n_units > U.nw;
 }
 
 int rc_launch_chain(const KeyTables *d_tables, StreamDesc desc, uint64_t n_streams,
                     ChainParams prm, uint64_t n_segs, const TileRecord *d_records,
                     uint64_t *d_cuts, int64_t *d_counts, uint64_t *d_scratch,
-                    uint64_t *d_seg_counts, bool any_multi, void *stream) {
+                    uint64_t *d_seg_counts, bool any_multi, uint32_t join, void *stream) {
     if (n_streams == 0) return 0;
     hipStream_t st = (hipStream_t)stream;
     // many single-segment streams with small windows and group bounds: one lane per stream
@@ -3021,8 +2918,8 @@ int rc_launch_chain(const KeyTables *d_tables, StreamDesc desc, uint64_t n_strea
     if (launch_status("rc_spec_kernel")) return 1;
     if (!any_multi) return 0;
     const uint64_t sgrid = (n_segs + 3) / 4, jgrid = (n_streams + kChainWaves - 1) / kChainWaves;
-    if (!rc_join_walk_only()) {
-        const bool repair = rc_repair_on();
+    if (!(join & RC_JOIN_WALK_ONLY)) {
+        const bool repair = (join & RC_JOIN_REPAIR) != 0;
         if (small)
             hipLaunchKernelGGL(rc_merge_kernel<1>, dim3((unsigned)sgrid), dim3(256), 0, st,
                                d_tables, desc, n_streams, prm, n_segs, d_records, d_scratch,
@@ -3059,23 +2956,23 @@ int rc_launch_chain(const KeyTables *d_tables, StreamDesc desc, uint64_t n_strea
     return launch_status("rc_join_kernel");
 }
 
-int rc_launch_read_probe(const uint8_t *d_src, uint64_t nbytes, uint32_t *d_out, void *stream) {
+int rc_launch_read_probe(const uint8_t *d_src, uint64_t nbytes, uint32_t *d_out, uint32_t block,
+                         void *stream) {
     const uint64_t n_tiles = nbytes / ((uint64_t)kTileKeys * 4);
     if (n_tiles == 0) return 0;
     uint64_t grid = (n_tiles + 15) / 16;
     const uint64_t cus = (uint64_t)cu_count();
     if (grid > cus) grid = cus;
-    uint64_t block = 0;  // RC_PROBE_BLOCK (diagnostics): interleaved runs of tiles, static
-    if (const char *e = getenv("RC_PROBE_BLOCK")) block = strtoull(e, nullptr, 0);
-    // otherwise the tile kernel's schedule (d_out[1] is the grab counter)
-    const TileUnits U = tile_units(n_tiles, grid * (1024 / kWaveSize));
+    // block (RC_PROBE_BLOCK, diagnostics): interleaved runs of tiles, static; otherwise the tile
+    // kernel's default schedule (d_out[1] is the grab counter)
+    const TileUnits U = tile_units(n_tiles, grid * (1024 / kWaveSize), TileSched{});
     if (block == 0 && U.n_units > U.nw &&
         hipMemsetAsync(d_out + 1, 0, sizeof(uint32_t), (hipStream_t)stream) != hipSuccess) {
         snprintf(g_launch_err, sizeof g_launch_err, "hipMemsetAsync failed");
         return 1;
     }
     hipLaunchKernelGGL(rc_read_probe_kernel, dim3((unsigned)grid), dim3(1024), 0,
-                       (hipStream_t)stream, d_src, n_tiles, d_out, block, U, d_out + 1);
+                       (hipStream_t)stream, d_src, n_tiles, d_out, (uint64_t)block, U, d_out + 1);
     return launch_status("rc_read_probe_kernel");
 }
 

@@ -13,7 +13,7 @@ What it replaces, in /root/reference/replicat/repository.py:
 The stream is gathered into host batches (``batch_bytes``, pinned) exactly as the batching shim
 does (replicat_amd/adapters.py): every batch but the last is chunked as an OPEN prefix (the
 reference's non-final ``next_cut`` calls), the last with its real framing, and the uncut tail
-is carried into the next batch.  ``slots`` batches (default 3) are in flight, each on its own
+is carried into the next batch.  ``slots`` batches (default 2) are in flight, each on its own
 HIP stream with its own digest / cipher handles: the files are read straight into one pinned
 batch (``readinto``) while the device works on the others, so the BLAKE2b floor of one batch
 (its longest chunk's chain, ~55 ms for a 5.12 MB chunk) overlaps the next
@@ -25,10 +25,22 @@ Only cut offsets, digests and -- what replicat uploads -- the chunk contents com
 from the host batch, or the device's nonce || C || T when encrypted.
 
 Memory held per producer: ``slots`` x (one pinned host batch + its HBM copy) of ``capacity`` =
-batch_bytes + max_length + 16 MiB + 128 bytes each (~1.02 GiB at the default 1 GiB batch, so ~3.1
-GiB pinned and ~3.1 GiB HBM with 3 slots); with ``encryption`` each slot also holds a pinned and
-an HBM ciphertext buffer of the same size plus 28 bytes per chunk (~6.1 GiB pinned in all).
-Smaller ``batch_bytes`` or ``slots`` shrink it linearly.
+batch_bytes + max_length + 16 MiB + 128 bytes each (~1.02 GiB at the default 1 GiB batch, so ~2.1
+GiB pinned and ~2.1 GiB HBM with the default 2 slots, ~3.1 with 3); with ``encryption`` each slot
+also holds a pinned and an HBM ciphertext buffer of the same size plus 28 bytes per chunk (~4.1
+GiB pinned in all with 2 slots).  Smaller ``batch_bytes`` or ``slots`` shrink it linearly.
+
+Two ways to consume the chunks:
+
+* ``run(paths)`` returns the whole ``SnapshotStream``; every ``ChunkRecord.contents`` is a copy
+  (bytes) made on the collector thread -- the host copies were ~0.46 s of an 8 GiB snapshot
+  (DESIGN.md §5c);
+* ``stream(paths)`` yields the ``ChunkRecord``s batch by batch as replicat's upload queue takes
+  ``_SnapshotChunk``s (repository.py:1492, :1507-1554), with ``contents`` a read-only
+  memoryview INTO the pinned batch (or the pinned ciphertexts): no copy.  The consumer calls
+  ``record.release()`` when it is done with the contents (an upload worker, after its upload); a
+  batch's pinned buffer is refilled only once every record of it has been released (or
+  garbage-collected), so a view never changes under its reader.
 
 The dedup table and the chunk -> file range map are host bookkeeping on a few integers per
 chunk, as in the reference.  Per-file digests of files of 1 MiB and more are hashed on host
@@ -69,16 +81,69 @@ class FileRecord:
     size: Optional[int] = None   # at open time (fstat of the opened file), when it tells
 
 
+class _Lease:
+    """Records of one batch whose contents still view its pinned buffer (stream())."""
+
+    def __init__(self):
+        self.n = 0
+        self.cv = threading.Condition()
+
+    def take(self, k):
+        with self.cv:
+            self.n += k
+
+    def drop(self):
+        with self.cv:
+            self.n -= 1
+            if self.n == 0:
+                self.cv.notify_all()
+
+    def wait(self, abort, warn_after=60.0):
+        """Until every record is released; False if `abort` (an Event) was set first.  A
+        consumer that keeps records without releasing them stalls the producer: say so once."""
+        t0, warned = time.monotonic(), False
+        with self.cv:
+            while self.n:
+                if abort.is_set():
+                    return False
+                self.cv.wait(0.05)
+                if not warned and time.monotonic() - t0 > warn_after:
+                    warned = True
+                    import warnings
+                    warnings.warn(f'DeviceSnapshotProducer.stream: {self.n} ChunkRecord(s) of a '
+                                  'batch still unreleased; the producer waits to refill its '
+                                  'buffer (release() each record when done with it)',
+                                  RuntimeWarning, stacklevel=2)
+        return True
+
+
 @dataclass
 class ChunkRecord:
     """repository.py:1477-1485 (_SnapshotChunk) without the upload location.  ``contents`` is
-    what replicat uploads: the chunk bytes, or nonce || C || T for an encrypted repository."""
+    what replicat uploads: the chunk bytes, or nonce || C || T for an encrypted repository --
+    bytes from run(), a read-only memoryview into the producer's pinned batch from stream()
+    (valid until release())."""
     counter: int
     stream_start: int
     stream_end: int
     digest: bytes
     table_index: int
-    contents: Optional[bytes] = field(default=None, repr=False)
+    contents: Optional[object] = field(default=None, repr=False)
+    _lease: Optional[_Lease] = field(default=None, repr=False, compare=False)
+
+    def release(self):
+        """Done with ``contents`` (a stream() record): its batch buffer may be refilled.
+        Idempotent; a record dropped without it releases when it is garbage-collected."""
+        lease, self._lease = self._lease, None
+        if lease is not None:
+            self.contents = None
+            lease.drop()
+
+    def __del__(self):
+        try:
+            self.release()
+        except Exception:  # interpreter shutdown
+            pass
 
 
 @dataclass
@@ -240,6 +305,7 @@ class _Slot:
             self.kdf_hasher = GpuBlake2b(length=prod.digest_size, device=prod.device)
             self.cipher = GpuAesGcm(key_bits=prod.encryption.key_bits,
                                     nonce_bits=prod.encryption.nonce_bits, device=prod.device)
+        self.lease = _Lease()  # stream(): records still viewing host / h_enc
         self.reset(prod.head)
 
     def close(self):
@@ -267,7 +333,7 @@ class DeviceSnapshotProducer:
                  params: Optional[bytes] = None, digest_size: int = 64,
                  batch_bytes: int = DEFAULT_BATCH, device=None, keep_contents: bool = True,
                  encryption: Optional[ChunkEncryption] = None, file_digests: str = 'auto',
-                 slots: int = 3):
+                 slots: int = 2):
         import torch
         if device is None:
             device = _current_device()
@@ -372,21 +438,35 @@ class DeviceSnapshotProducer:
     # ------------------------------------------------------------------------------ run
 
     def run(self, paths: Sequence[os.PathLike], read=None) -> SnapshotStream:
+        """The whole snapshot stream, every chunk's contents copied out (bytes)."""
+        files: List[FileRecord] = []
+        run = self._produce(paths, read, files, zero_copy=False, sink=None,
+                            abort=threading.Event())
+        return SnapshotStream(files=files, chunks=run.chunks, chunks_table=run.table)
+
+    def stream(self, paths: Sequence[os.PathLike], read=None) -> 'ChunkStream':
+        """The chunks as they are produced (a ``ChunkStream``: iterate it for ``ChunkRecord``s
+        whose ``contents`` view the pinned batches -- release() each when done), produced on a
+        thread of its own like replicat's chunk-producer thread (repository.py:1358,1556)."""
+        return ChunkStream(self, paths, read)
+
+    def _produce(self, paths, read, files, zero_copy, sink, abort):
         """Batch k + 1 is read from the files while the device cuts and digests batch k, and
         batch k's records are built while the device works on batch k + 1.  The uncut tail of
         batch k (known once its cut chain is done, long before its digests) is copied to the
-        head of batch k + 1 on the host, so every batch is uploaded once."""
+        head of batch k + 1 on the host, so every batch is uploaded once.  zero_copy: records
+        view the slot (sink(records) gets every batch's; the slot is refilled once all are
+        released)."""
         import torch
         if not self._slots:
             raise RuntimeError('DeviceSnapshotProducer is closed')
-        files: List[FileRecord] = []
-        run = _Run(self, torch, files)
+        run = _Run(self, torch, files, zero_copy, sink)
         reader = PieceReader(sort_files(paths), files, read, record=FileRecord, on_open=_fstat_size)
         # fill / wait_cut / enqueue / collect_join: this thread; collect_wait / records /
         # host_digest_wait: the collector thread (overlapping the next fill)
         prof = self.profile = {'fill': 0.0, 'wait_cut': 0.0, 'enqueue': 0.0, 'collect_join': 0.0,
                                'collect_wait': 0.0, 'records': 0.0, 'host_digest_wait': 0.0,
-                               'batches': 0}
+                               'release_wait': 0.0, 'batches': 0}
         clock = time.perf_counter
         prev, look, k = None, None, 0
         # records are built on a collector thread (they copy chunk contents, holding the GIL)
@@ -403,6 +483,11 @@ class DeviceSnapshotProducer:
                     collected[k % ns].result()
                     collected[k % ns] = None
                     prof['collect_join'] += clock() - t
+                # and every stream() record viewing its bytes released (also across runs)
+                t = clock()
+                if not s.lease.wait(abort):
+                    raise _Aborted()
+                prof['release_wait'] += clock() - t
                 s.reset(self.head)
                 # ---- fill: the piece read ahead, then whole pieces up to batch_bytes of new bytes
                 t0 = clock()
@@ -457,16 +542,17 @@ class DeviceSnapshotProducer:
                     sl.host_jobs.wait()
                 except BaseException:
                     pass
-        return SnapshotStream(files=files, chunks=run.chunks, chunks_table=run.table)
+        return run
 
 
 class _Run:
     """The bookkeeping of one DeviceSnapshotProducer.run: per-file digest states and engines,
     the dedup table, the chunk records."""
 
-    def __init__(self, prod, torch, files):
+    def __init__(self, prod, torch, files, zero_copy=False, sink=None):
         self.p, self.torch, self.files = prod, torch, files
-        self.chunks: List[ChunkRecord] = []
+        self.zero_copy, self.sink = zero_copy, sink
+        self.chunks: List[ChunkRecord] = []  # zero_copy: records without contents
         self.table: Dict[bytes, int] = {}
         self.states = {}     # file index -> device state (open device-engine files)
         self.hstates = {}    # file index -> _HostHash (host-engine files)
@@ -576,6 +662,10 @@ class _Run:
         t1 = clock()
         prof['collect_wait'] += t1 - t0
         chunks, table, hnp = self.chunks, self.table, s.hnp
+        zc = self.zero_copy and p.keep_contents
+        # zero copy: read-only views into the pinned batch (or ciphertexts), leased per batch
+        view = memoryview(enc if enc is not None else hnp).toreadonly() if zc else None
+        out = [] if self.sink is not None else None
         prev = 0
         for k, e in enumerate(ends.tolist()):
             d = digs[k].tobytes()
@@ -584,13 +674,25 @@ class _Run:
                 idx = table[d] = len(table)
             if enc is not None:  # nonce || C || T of chunk k at prev + k (nonce_bytes + 16)
                 o = prev + k * over
-                contents = enc[o:o + (e - prev) + over].tobytes()
+                contents = view[o:o + (e - prev) + over] if zc else enc[o:o + (e - prev) + over].tobytes()
+            elif not p.keep_contents:
+                contents = None
             else:
-                contents = hnp[s.off + prev:s.off + e].tobytes() if p.keep_contents else None
-            chunks.append(ChunkRecord(counter=len(chunks) + 1, stream_start=s.buf_start + prev,
-                                      stream_end=s.buf_start + e, digest=d, table_index=idx,
-                                      contents=contents))
+                contents = view[s.off + prev:s.off + e] if zc else hnp[s.off + prev:s.off + e].tobytes()
+            rec = ChunkRecord(counter=len(chunks) + 1, stream_start=s.buf_start + prev,
+                              stream_end=s.buf_start + e, digest=d, table_index=idx,
+                              contents=None if zc else contents)
+            chunks.append(rec)
+            if out is not None:
+                if zc:  # the consumer's copy of the record carries the view and the lease
+                    rec = ChunkRecord(rec.counter, rec.stream_start, rec.stream_end, d, idx,
+                                      contents, s.lease)
+                out.append(rec)
             prev = e
+        if out is not None:
+            if zc:
+                s.lease.take(len(out))
+            self.sink(out)
         t2 = clock()
         prof['records'] += t2 - t1
         s.host_jobs.wait()  # every host piece of this slot, before it is refilled
@@ -604,10 +706,93 @@ class _Run:
             raise RuntimeError(f'final batch left {s.blen - prev} bytes uncut')
 
 
+class _Aborted(Exception):
+    """The consumer of a ChunkStream went away: the producer thread stops."""
+
+
+class ChunkStream:
+    """The chunks of one snapshot, produced on a thread of its own (DeviceSnapshotProducer
+    .stream): iterate it for ``ChunkRecord``s in stream order; ``contents`` views the producer's
+    pinned batch until ``release()``.  Once exhausted, ``files`` and ``chunks_table`` are the
+    run's (``snapshot()`` gives the ``SnapshotStream``, records without contents).  ``close()``
+    (also on leaving a ``with`` block, or when iteration is abandoned) stops the producer."""
+
+    _END = object()
+
+    def __init__(self, prod, paths, read=None):
+        import queue
+        self.files: List[FileRecord] = []
+        self._q = queue.Queue()
+        self._abort = threading.Event()
+        self._run = None
+        self._done = False
+
+        def work():
+            try:
+                self._run = prod._produce(paths, read, self.files, zero_copy=True,
+                                          sink=self._q.put, abort=self._abort)
+                self._q.put(self._END)
+            except _Aborted:
+                self._q.put(self._END)
+            except BaseException as e:  # re-raised in the consumer
+                self._q.put(e)
+
+        self._thread = threading.Thread(target=work, name='rc-chunk-producer', daemon=True)
+        self._thread.start()
+
+    def __iter__(self):
+        while not self._done:
+            item = self._q.get()
+            if item is self._END:
+                self._done = True
+                self._thread.join()
+                return
+            if isinstance(item, BaseException):
+                self._done = True
+                self._thread.join()
+                raise item
+            yield from item
+
+    @property
+    def chunks_table(self):
+        return self._run.table if self._run is not None else {}
+
+    def snapshot(self) -> SnapshotStream:
+        if not self._done or self._run is None:
+            raise RuntimeError('ChunkStream not exhausted')
+        return SnapshotStream(files=self.files, chunks=self._run.chunks,
+                              chunks_table=self._run.table)
+
+    def close(self):
+        if self._thread.is_alive():
+            self._abort.set()
+            while self._thread.is_alive():  # drain (drops unconsumed records, releasing them)
+                try:
+                    item = self._q.get(timeout=0.05)
+                except Exception:
+                    continue
+                del item
+            self._thread.join()
+        self._done = True
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def snapshot_stream(paths, **kw) -> SnapshotStream:
     """One-shot helper: DeviceSnapshotProducer(**kw).run(paths)."""
     return DeviceSnapshotProducer(**kw).run(paths)
 
 
-__all__ = ['DeviceSnapshotProducer', 'SnapshotStream', 'FileRecord', 'ChunkRecord', 'ChunkEncryption',
-           'snapshot_stream', 'DEFAULT_BATCH']
+__all__ = ['DeviceSnapshotProducer', 'SnapshotStream', 'ChunkStream', 'FileRecord', 'ChunkRecord',
+           'ChunkEncryption', 'snapshot_stream', 'DEFAULT_BATCH']

@@ -54,10 +54,12 @@ for s in settings:
     elif seg != '0':
         os.environ['RC_SEGMENT_BYTES'] = seg
     os.environ['RC_SEGMENT_EXT'] = ext
-    chs[s] = GpuChunker(128_000, 5_120_000, b'\xff' * 16)
+    os.environ['RC_REPAIR'] = '0' if s.endswith(':norepair') else '1'
+    chs[s] = GpuChunker(128_000, 5_120_000, b'\xff' * 16)  # knobs read at creation (knobs.h)
 os.environ.pop('RC_SEGMENT_BYTES', None)
 os.environ.pop('RC_SEGMENT_EXT', None)
 os.environ.pop('RC_SEGMENT_FLOOR', None)
+os.environ.pop('RC_REPAIR', None)
 total, caps = chs[settings[0]].capacity([size] * n)
 base = np.concatenate([[0], np.cumsum(caps)[:-1]]).astype(np.int64)
 cuts = torch.zeros(total, dtype=torch.int64, device='cuda')
@@ -69,7 +71,6 @@ res = {s: [] for s in settings}
 for r in range(rounds):
     for s in (settings if r % 2 == 0 else settings[::-1]):
         ch = chs[s]
-        os.environ['RC_REPAIR'] = '0' if s.endswith(':norepair') else '1'  # read per launch
         ch.chunk_device(ptrs, [size] * n, last, cuts.data_ptr(), counts.data_ptr(), hs)
         torch.cuda.synchronize()
         ch.timing(True)

@@ -1,7 +1,7 @@
 """Diagnostic: what config 3 (iii)'s tile kernel pays for, on ONE 64 GiB arena in one process:
 the same bytes as 65,536 x 1 MiB streams (3 iii) or 1024 x 64 MiB, each with a small-window
 chunker (min 2,000 / max 80,000) that writes group records (rc_tile_kernel<4>, the default for
-such windows) and one built with RC_TILE_GROUPS_OFF=1 (rc_tile_kernel<1>); settings alternate
+such windows) and one built with RC_TILE_GROUPS=0 (rc_tile_kernel<1>); settings alternate
 round after round, tile-kernel time by HIP events (sequential calls).
 
     python scripts/groups_ab.py [rounds]
@@ -25,9 +25,9 @@ pool = torch.empty(total + 64, dtype=torch.uint8, device='cuda')
 fill_splitmix_streams(pool.data_ptr(), 65536, 1 << 20, 1 << 20, synth.DEFAULT_SEED, 0, 1, hs)
 layouts = {'3iii_1MiB': (65536, 1 << 20), 'long_64MiB': (1024, 64 << 20)}
 chs = {'groups': GpuChunker(2_000, 80_000, b'\xff' * 16)}
-os.environ['RC_TILE_GROUPS_OFF'] = '1'
+os.environ['RC_TILE_GROUPS'] = '0'
 chs['nogroups'] = GpuChunker(2_000, 80_000, b'\xff' * 16)
-os.environ.pop('RC_TILE_GROUPS_OFF')
+os.environ.pop('RC_TILE_GROUPS')
 res = {}
 for r in range(rounds):
     for lay, (n, size) in layouts.items():

@@ -5,7 +5,8 @@ median wall time per step over K back-to-back steps, the tile kernel's HIP-event
 edge + chain time are printed.  Every setting must give the same cut lists.
 
     python scripts/overlap_ab.py [config] [rounds] [setting ...]   setting = seq | pR (R CUs)
-                                          [:full] [@STATIC:CHUNK] (tile schedule, per launch)
+                                          [@STATIC:CHUNK] (tile schedule: a chunker created
+                                          with RC_TILE_STATIC / RC_TILE_CHUNK, knobs.h)
     python scripts/overlap_ab.py 2 4 seq p8 p16 p32
 """
 import json
@@ -47,7 +48,28 @@ else:
     fill_splitmix_streams(pool.data_ptr(), n, size, size, synth.DEFAULT_SEED, 0, 1, hs)
     ptrs = np.arange(n, dtype=np.uint64) * size + pool.data_ptr()
     lens, last = [size] * n, ([size - (1 << 20)] if cfg == '3ii' else None)
-ch = GpuChunker(mn, mx, b'\xff' * 16)
+
+
+def chunker_with(env):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return GpuChunker(mn, mx, b'\xff' * 16)  # knobs are read here
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k)
+            else:
+                os.environ[k] = v
+
+
+chunkers = {}
+for s in settings:
+    sched = s.partition('@')[2]
+    if sched not in chunkers:
+        st, ck = sched.split(':') if sched else (None, None)
+        chunkers[sched] = chunker_with({'RC_TILE_STATIC': st, 'RC_TILE_CHUNK': ck} if sched else {})
+ch = next(iter(chunkers.values()))
 total, caps = ch.capacity(lens)
 cuts = torch.zeros(total, dtype=torch.int64, device='cuda')
 counts = torch.zeros(len(lens), dtype=torch.int64, device='cuda')
@@ -60,15 +82,9 @@ res = {s: [] for s in settings}
 for r in range(rounds):
     order = settings if r % 2 == 0 else settings[::-1]
     for s in order:
-        base, _, sched = s.partition('@')  # ...@STATIC:CHUNK -- the tile schedule (per launch)
-        if sched:
-            os.environ['RC_TILE_STATIC'], os.environ['RC_TILE_CHUNK'] = sched.split(':')
-        else:
-            os.environ.pop('RC_TILE_STATIC', None)
-            os.environ.pop('RC_TILE_CHUNK', None)
+        base, _, sched = s.partition('@')  # ...@STATIC:CHUNK -- the tile schedule's chunker
+        ch = chunkers[sched]
         pipe = base != 'seq'
-        # pR:full -- the first version's extra event packets between tile kernels (RC_PIPE_LEAN=0)
-        os.environ['RC_PIPE_LEAN'] = '0' if base.endswith(':full') else '1'
         if pipe:
             ch.overlap(int(base[1:].split(':')[0]))
 
@@ -105,4 +121,5 @@ for s, v in res.items():
               'GiBps': round(float(np.sum(lens)) / (med[0] * 1e-3) / 2**30, 1)}
 print(json.dumps(out), flush=True)
 torch.cuda.synchronize()
-ch.close()  # the CU-masked streams go while the runtime is up
+for c in chunkers.values():
+    c.close()  # the CU-masked streams go while the runtime is up (the library would at exit)

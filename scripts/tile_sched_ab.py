@@ -1,14 +1,15 @@
 """A/B of the tile kernel's work-unit schedule on ONE allocation (the per-allocation read-rate
 spread of profiles/r02/placement is larger than the effect, so settings are compared inside one
-process on one arena).  The schedule is read per launch from RC_TILE_STATIC (per mille of the
+process on one arena).  Each setting is a chunker created with RC_TILE_STATIC (per mille of the
 tiles handed out statically; 1000 = fully static, the round-2 schedule) and RC_TILE_CHUNK (tiles
-per dynamic unit); settings alternate round after round and the median tile-kernel time per
-setting is printed.
+per dynamic unit) in the environment -- the library reads its knobs when a chunker is created
+(replicat_amd/csrc/knobs.h); settings alternate round after round and the median tile-kernel
+time per setting is printed.
 
     python scripts/tile_sched_ab.py [config] [rounds] [setting ...]  setting = STATIC:CHUNK[:g]
     python scripts/tile_sched_ab.py 2 6 1000:32 750:32 500:16 500:64
 
-A trailing ":g" runs that setting on a chunker created with RC_TILE_GROUPS_ON=1 (group records
+A trailing ":g" runs that setting on a chunker created with RC_TILE_GROUPS=1 (group records
 and edge-range trimming for large windows too).
 """
 import json
@@ -45,11 +46,30 @@ else:
     fill_splitmix_streams(pool.data_ptr(), n, size, size, synth.DEFAULT_SEED, 0, 1, hs)
     ptrs = np.arange(n, dtype=np.uint64) * size + pool.data_ptr()
     lens, last = [size] * n, None
-ch0 = GpuChunker(mn, mx, b'\xff' * 16)
-os.environ['RC_TILE_GROUPS_ON'] = '1'
-chg = GpuChunker(mn, mx, b'\xff' * 16)
-os.environ.pop('RC_TILE_GROUPS_ON')
-total, caps = ch0.capacity(lens)
+
+
+
+def chunker_with(env):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return GpuChunker(mn, mx, b'\xff' * 16)  # knobs are read here
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k)
+            else:
+                os.environ[k] = v
+
+
+chunkers = {}
+for s in settings:
+    st, ck = s.split(':')[:2]
+    env = {'RC_TILE_STATIC': st, 'RC_TILE_CHUNK': ck}
+    if s.endswith(':g'):
+        env['RC_TILE_GROUPS'] = '1'
+    chunkers[s] = chunker_with(env)
+total, caps = chunkers[settings[0]].capacity(lens)
 cuts = torch.zeros(total, dtype=torch.int64, device='cuda')
 counts = torch.zeros(len(lens), dtype=torch.int64, device='cuda')
 ptrs = np.ascontiguousarray(ptrs, dtype=np.uint64)
@@ -60,9 +80,7 @@ res = {s: [] for s in settings}
 for r in range(rounds):
     order = settings if r % 2 == 0 else settings[::-1]
     for s in order:
-        st, ck = s.split(':')[:2]
-        ch = chg if s.endswith(':g') else ch0
-        os.environ['RC_TILE_STATIC'], os.environ['RC_TILE_CHUNK'] = st, ck
+        ch = chunkers[s]
         for _ in range(2):
             ch.chunk_device(ptrs, lens, last, cuts.data_ptr(), counts.data_ptr(), hs)
         torch.cuda.synchronize()

@@ -416,6 +416,152 @@ def make_config4(procs=4):
             'per_gpu': per_gpu}
 
 
+# ------------------------------ every rank's own shard of a multi-GPU line (ranks.json)
+
+RANKS, RANK_STREAMS, RANK_SIZE = 8, 1024, 64 << 20
+RANK_SEEDED = 128                     # the seeded key's streams per shard (encrypted leg)
+RANK_3III, RANK_3III_SIZE = 65536, 1 << 20
+
+
+def _ref_cut(data, mn, mx, key):
+    """The REFERENCE's ``next_cut`` over one single-piece stream exactly as its adapter calls it
+    (adapters.py:290-305: every call final, the buffer the uncut rest), on a zero-copy view."""
+    ch = REF_EXT._gclmulchunker(mn, mx, key)
+    mv, size = memoryview(data), len(data)
+    pos, ends = 0, []
+    while pos < size:
+        c = ch.next_cut(mv[pos:], True)
+        if not c:
+            break
+        pos += c
+        ends.append(pos)
+    return ends
+
+
+def _rank_stream(sid, size):
+    import numpy as np
+    from oracle import oracle as o
+    data = np.empty(size, dtype=np.uint8)
+    o.lib().oc_fill_splitmix(data.ctypes.data, size, synth.DEFAULT_SEED, sid)
+    return data
+
+
+def _rank_job(job):
+    """One config-2-shaped stream of a rank's shard: its cut list under the unencrypted key and
+    its chunks' BLAKE2b-512 digests (config 5's content identity, repository.py:1462); with
+    ``edit`` the edited copy instead; with ``key`` the cut list under that key only."""
+    import hashlib as _h
+    kind, sid, size, mn, mx, key, edit = job
+    data = _rank_stream(sid, size)
+    if edit is not None:
+        data = synth.apply_edit(data, edit[0], edit[1], bytes.fromhex(edit[2]))
+    ends = _ref_cut(data, mn, mx, b'\xff' * 16 if key is None else bytes.fromhex(key))
+    digests = []
+    if kind == 'digests':
+        raw, start = memoryview(data), 0
+        for e in ends:
+            digests.append(_h.blake2b(raw[start:e]).digest())
+            start = e
+    return sid, ends, digests
+
+
+def rank_edit_plan(rank, n=RANK_STREAMS, size=RANK_SIZE):
+    """Config 5's edits on rank ``rank``'s shard (local stream indices): rank 0's plan is the
+    single-GPU one (seed 5, large.json); rank r uses seed 5 + r.  bench.Config5 uses the same."""
+    return synth.edit_plan(n, n // 2, size, seed=5 + rank)
+
+
+def make_ranks(procs=8):
+    """Per-rank fixtures for multi-GPU lines (bench.shard_ids: rank r chunks streams
+    r*n .. r*n + n - 1): config 2 under key ff (the whole shard), the seeded key (the shard's
+    first 128 streams), config 5 (the shard's own edit plan and dedup against the shard) and
+    config 3 (iii) (65,536 x 1 MiB per rank), all cut by the reference's ``next_cut``.  Rank 0's
+    entries must equal the single-GPU fixtures (digests.json, large.json): checked here."""
+    seeded = synth.seeded_key(1).hex()
+    out = {'ranks': RANKS, 'seed': synth.DEFAULT_SEED, 'min': MIN_DEF, 'max': MAX_DEF,
+           'config2_ff': [], 'config2_seeded': [], 'config5': [], 'config3iii': []}
+    with mp.get_context('fork').Pool(procs) as pool:
+        for r in range(RANKS):
+            ids = [r * RANK_STREAMS + i for i in range(RANK_STREAMS)]
+            res = sorted(pool.map(_rank_job, [('digests', s, RANK_SIZE, MIN_DEF, MAX_DEF, None,
+                                               None) for s in ids], chunksize=4))
+            ends = [e for _, e, _ in res]
+            known = {d for _, _, ds in res for d in ds}
+            out['config2_ff'].append({'rank': r, 'first_id': ids[0], 'streams': len(ids),
+                                      'chunks': sum(map(len, ends)),
+                                      'sha256': cutlist_digest(ends)})
+            sd = sorted(pool.map(_rank_job, [('cuts', s, RANK_SIZE, MIN_DEF, MAX_DEF, seeded,
+                                              None) for s in ids[:RANK_SEEDED]], chunksize=2))
+            out['config2_seeded'].append({'rank': r, 'first_id': ids[0], 'streams': RANK_SEEDED,
+                                          'params': seeded,
+                                          'chunks': sum(len(e) for _, e, _ in sd),
+                                          'sha256': cutlist_digest([e for _, e, _ in sd])})
+            plan = rank_edit_plan(r)
+            jobs = [('digests', ids[loc], RANK_SIZE, MIN_DEF, MAX_DEF, None,
+                     (kind, off, payload.hex())) for loc, kind, off, payload in plan]
+            ed = sorted(pool.map(_rank_job, jobs, chunksize=2))
+            dup = total = 0
+            for _, e_ends, e_dig in ed:
+                start = 0
+                for e, dg in zip(e_ends, e_dig):
+                    if dg in known:
+                        dup += e - start
+                    start = e
+                total += e_ends[-1]
+            out['config5'].append({'rank': r, 'plan_seed': 5 + r, 'edited': len(plan),
+                                   'original_sha256': out['config2_ff'][-1]['sha256'],
+                                   'edited_sha256': cutlist_digest([e for _, e, _ in ed]),
+                                   'dup_bytes_edited': dup, 'total_bytes_edited': total})
+            ids3 = [r * RANK_3III + i for i in range(RANK_3III)]
+            e3 = sorted(pool.map(_rank_job, [('cuts', s, RANK_3III_SIZE, 2_000, 80_000, None, None)
+                                             for s in ids3], chunksize=256))
+            out['config3iii'].append({'rank': r, 'first_id': ids3[0], 'streams': RANK_3III,
+                                      'chunks': sum(len(e) for _, e, _ in e3),
+                                      'sha256': cutlist_digest([e for _, e, _ in e3])})
+            print('rank', r, out['config2_ff'][-1]['sha256'][:16],
+                  out['config2_seeded'][-1]['sha256'][:16], out['config5'][-1]['dup_bytes_edited'],
+                  out['config3iii'][-1]['sha256'][:16], flush=True)
+    with open(os.path.join(HERE, 'digests.json')) as f:
+        single = {d['name']: d for d in json.load(f)}
+    with open(os.path.join(HERE, 'large.json')) as f:
+        c5 = {d['name']: d for d in json.load(f)}['config5']
+    assert out['config2_ff'][0]['sha256'] == single['config2_ff']['sha256']
+    assert out['config2_seeded'][0]['sha256'] == single['config2_seeded_first128']['sha256']
+    assert out['config3iii'][0]['sha256'] == single['config3iii']['sha256']
+    assert (out['config5'][0]['edited_sha256'], out['config5'][0]['dup_bytes_edited'],
+            out['config5'][0]['total_bytes_edited']) == (c5['edited_sha256'],
+                                                         c5['dup_bytes_edited'],
+                                                         c5['total_bytes_edited'])
+    return out
+
+
+def make_ranks_small(n=2, size=16 << 20):
+    """A small config-2-shaped shard per rank (n streams of 16 MiB, default parameters, key ff,
+    streams r*n ..): what the CPU tests' stand-in ranks chunk, so that every rank of a world-2
+    line carries a flag there too."""
+    per_rank = []
+    for r in range(RANKS):
+        ends = [_ref_cut(_rank_stream(r * n + i, size), MIN_DEF, MAX_DEF, b'\xff' * 16)
+                for i in range(n)]
+        per_rank.append({'rank': r, 'first_id': r * n, 'chunks': sum(map(len, ends)),
+                         'sha256': cutlist_digest(ends)})
+    return {'streams': n, 'size': size, 'per_rank': per_rank}
+
+
+def _config3ii_world(world):
+    return make_config3ii(size=world * (64 << 30))
+
+
+def make_config3ii_worlds(worlds=(2, 4, 8)):
+    """Config 3 (ii) as bench.py runs it on `world` ranks: ONE stream of world x 64 GiB (last
+    piece the final 1 MiB) split over the ranks, the whole spliced list on every rank."""
+    with mp.get_context('fork').Pool(len(worlds)) as pool:
+        out = pool.map(_config3ii_world, worlds)
+    for w, d in zip(worlds, out):
+        d['world'] = w
+    return out
+
+
 # ------------------------------------- the reference's benchmark harness (harness.json)
 
 def make_harness():
@@ -519,6 +665,26 @@ def main():
             sets = [s for s in json.load(f) if s['name'] != 'config3iii']
         with open(path, 'w') as f:
             json.dump(sets + [d], f, separators=(',', ':'))
+            f.write('\n')
+        return
+    if '--ranks-extra' in sys.argv:
+        # the small per-rank shards and config 3 (ii) at 2 / 4 / 8 ranks, added to ranks.json
+        path = os.path.join(HERE, 'ranks.json')
+        with open(path) as f:
+            d = json.load(f)
+        d['small'] = make_ranks_small()
+        if '--no-3ii' not in sys.argv:
+            d['config3ii'] = make_config3ii_worlds()
+            for c in d['config3ii']:
+                print('config3ii world', c['world'], c['chunks'], c['sha256'][:16], flush=True)
+        with open(path, 'w') as f:
+            json.dump(d, f, indent=1)
+            f.write('\n')
+        return
+    if '--ranks' in sys.argv:
+        d = make_ranks()
+        with open(os.path.join(HERE, 'ranks.json'), 'w') as f:
+            json.dump(d, f, indent=1)
             f.write('\n')
         return
     if '--config4' in sys.argv:

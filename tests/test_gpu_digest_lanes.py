@@ -1,6 +1,6 @@
 """The one-lane-per-chunk form of the BLAKE2b digests (blake2b.hip lane_hash): the same hashlib
 checks as tests/test_gpu_digest.py with the lane / quad split forced through RC_B2_LANE_MAX and
-RC_B2_LANE_ONLY (read per call): every item by the lane kernel (rc_b2_lane_kernel), every item by
+RC_B2_LANE_ONLY (read when the hasher is created): every item by the lane kernel (rc_b2_lane_kernel), every item by
 the fused kernel's lane role (rc_b2_kernel), a mixed split, and the default split on batches of
 many short chunks (config 3 iii's parameters): a mixed one and a lane-only one."""
 
@@ -32,8 +32,9 @@ def split(request, monkeypatch):
     return request.param
 
 
-@pytest.fixture(scope='module')
-def hasher():
+@pytest.fixture
+def hasher(split):
+    # the split knobs are read when a hasher is created (knobs.h): one per setting
     return GpuBlake2b(length=64)
 
 
@@ -64,13 +65,14 @@ def test_chunk_digests_lanes(split, hasher, mn, mx):
 
 
 @pytest.mark.parametrize('n', [8192, 16384])
-def test_many_short_chunks_default_split(hasher, monkeypatch, n):
+def test_many_short_chunks_default_split(monkeypatch, n):
     """n x 1 MiB streams at min 2,000 / max 80,000, throughput-bound (>= 80,000 << 16 bytes): at
     8 GiB the default split sends chunks of up to 64 KiB to lanes and the rest to quads (the
     fused kernel); at 16 GiB every chunk fits a lane (up to 128 KiB: the lane kernel).  Every
     chunk of a sample of streams = hashlib."""
     monkeypatch.delenv('RC_B2_LANE_MAX', raising=False)
     monkeypatch.delenv('RC_B2_LANE_ONLY', raising=False)
+    hasher = GpuBlake2b(length=64)  # the default split (knobs read at creation)
     size = 1 << 20
     ch = GpuChunker(2_000, 80_000, b'\xff' * 16)
     ts, res = D._chunk_and_digest(ch, hasher, [size] * n)

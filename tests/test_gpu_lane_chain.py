@@ -94,8 +94,8 @@ def test_lane_chain_many_streams_default_switch(monkeypatch):
     n, size = 2048, 256 << 10
     ts = device_streams([size] * n, seed=synth.DEFAULT_SEED, ids=list(range(4000, 4000 + n)))
     got = chunk_device(ch, ts, [size] * n)
-    monkeypatch.setenv('RC_LANE_CHAIN', '0')
-    ref = chunk_device(ch, ts, [size] * n)
+    monkeypatch.setenv('RC_LANE_CHAIN', '0')  # read when a chunker is created (knobs.h)
+    ref = chunk_device(GpuChunker(mn, mx, b'\xff' * 16), ts, [size] * n)
     assert got == ref
     for i in range(0, n, 97):
         d = ts[i][:size].cpu().numpy()

@@ -196,3 +196,106 @@ def test_close_and_context_manager(tmp_path):
         check_stream(prod.run(paths), files_data)
     with pytest.raises(RuntimeError, match='closed'):
         prod.run(paths)
+
+
+# ------------------------------------------------------------- stream(): zero-copy records
+
+def _streamed(prod, paths, hold=0, workers=0):
+    """Consume prod.stream(paths) the way replicat's upload workers take _SnapshotChunks
+    (repository.py:1492, 1507-1554): each record's contents are checked against its digest at
+    the moment it is 'uploaded', then released.  hold: records kept unreleased in a FIFO (an
+    upload queue) before the oldest is handled; workers > 0: handled on that many threads."""
+    import collections
+    import concurrent.futures as cf
+    out, held, bad = [], collections.deque(), []
+
+    plain = prod.encryption is None  # encrypted contents are nonce || C || T
+
+    def upload(rec):
+        data = bytes(rec.contents)
+        if plain and hashlib.blake2b(data).digest() != rec.digest:
+            bad.append(rec.counter)
+        rec.release()
+        return rec.counter, data
+
+    pool = cf.ThreadPoolExecutor(workers) if workers else None
+    futs = []
+    with prod.stream(paths) as st:
+        for rec in st:
+            assert isinstance(rec.contents, memoryview) and rec.contents.readonly
+            held.append(rec)
+            while len(held) > hold:
+                r = held.popleft()
+                if pool:
+                    futs.append(pool.submit(upload, r))
+                else:
+                    out.append(upload(r))
+        while held:
+            out.append(upload(held.popleft()))
+        res = st.snapshot()
+    if pool:
+        out += [f.result() for f in futs]
+        pool.shutdown()
+    assert not bad, bad[:5]
+    data = dict(out)
+    for c in res.chunks:  # the run's records carry no contents: give them the uploaded bytes
+        assert c.contents is None
+        c.contents = data[c.counter]
+    return res
+
+
+@pytest.mark.parametrize('name', sorted(SNAPS))
+@pytest.mark.parametrize('hold,workers', [(0, 0), (40, 0), (8, 4)])
+def test_stream_reference_snapshots(tmp_path, name, hold, workers):
+    """stream() gives the reference's chunks, digests and file ranges with views into the
+    pinned batches; records held across batch boundaries (hold) or released on other threads
+    (workers) never see a refilled buffer."""
+    s = SNAPS[name]
+    files_data = file_sets()[name]
+    paths = write(tmp_path, files_data)
+    params = None if s['params'] is None else bytes.fromhex(s['params'])
+    prod = DeviceSnapshotProducer(min_length=s['min'], max_length=s['max'], params=params,
+                                  batch_bytes=1 << 20)
+    res = _streamed(prod, paths, hold, workers)
+    check_stream(res, files_data, s['lengths'])
+    # the same producer again, now through run(): the same stream
+    again = prod.run(paths)
+    assert [(c.stream_end, c.digest) for c in again.chunks] == \
+        [(c.stream_end, c.digest) for c in res.chunks]
+
+
+def test_stream_encrypted_and_abandoned(oracle, tmp_path):
+    """Encrypted records view the pinned ciphertexts (nonce || C || T, decrypted by the oracle
+    under the chunk's subkey); a consumer that stops early (close()) leaves the producer
+    usable for the next stream."""
+    from replicat_amd.pipeline import ChunkEncryption
+    rnd = random.Random(1470)
+    files_data = {'f%02d' % i: rnd.randbytes(rnd.choice([7, 4096, rnd.randrange(0, 3_000_000)]))
+                  for i in range(16)}
+    paths = write(tmp_path, files_data)
+    enc = ChunkEncryption(shared_key=rnd.randbytes(32), shared_kdf_params=rnd.randbytes(16))
+    mn, mx = 2_000, 80_000
+    prod = DeviceSnapshotProducer(min_length=mn, max_length=mx, batch_bytes=1 << 20,
+                                  encryption=enc)
+    stream = b''.join(snapshot.stream_pieces(snapshot.sort_files(paths)))
+    n = 0
+    with prod.stream(paths) as st:
+        for rec in st:
+            plain = stream[rec.stream_start:rec.stream_end]
+            subkey = hashlib.blake2b(rec.digest, salt=enc.shared_kdf_params, key=enc.shared_key,
+                                     digest_size=32).digest()
+            blob = bytes(rec.contents)
+            assert oracle.gcm_decrypt(subkey, blob[:12], blob[12:]) == plain
+            rec.release()
+            n += 1
+            if n == 40:
+                break  # abandoned: the producer thread stops at its next batch
+    assert n == 40
+    res = _streamed(prod, paths, hold=5)
+    assert res.chunks[-1].stream_end == len(stream)
+    for c in res.chunks:
+        blob = c.contents
+        subkey = hashlib.blake2b(c.digest, salt=enc.shared_kdf_params, key=enc.shared_key,
+                                 digest_size=32).digest()
+        assert oracle.gcm_decrypt(subkey, blob[:12], blob[12:]) == \
+            stream[c.stream_start:c.stream_end]
