@@ -130,6 +130,18 @@ uint64_t rc_chunker_pipelined_calls(const rc_chunker *ch);
  * made so far -- pipelined or not -- has written its cuts and counts. */
 int rc_chunk_wait(rc_chunker *ch, void *hip_stream);
 
+/* A HIP stream on `device` with a hardware queue of its own (no reference counterpart:
+ * plumbing for device-side overlap).  Plain HIP streams share the process's GPU_MAX_HW_QUEUES
+ * hardware queues (4 by default) and a kernel queued behind another stream's long kernel on the
+ * same queue waits for it; a stream created with a CU mask never shares its queue, so this one is
+ * created with every CU in its mask (hipExtStreamCreateWithCUMask).  Like every CU-masked stream
+ * it is a BLOCKING stream: work on the legacy NULL stream synchronises with it.  The snapshot
+ * producer's batch streams use it so that consecutive batches' digests (each ending with a
+ * ~55 ms BLAKE2b chain) overlap at HIP's default queue count.  rc_stream_destroy waits for the
+ * stream's work; streams still alive at process exit are destroyed then. */
+int rc_stream_create(int device, void **out_stream);
+void rc_stream_destroy(void *stream);
+
 /* The same over HOST-resident streams, blocking: pinned double-buffered H2D copies overlap
  * the kernels of the previous batch; cuts come back to host arrays laid out as above
  * (cuts[cut_base[i] ..], counts[i]).  This is the end-to-end path of DESIGN.md. */

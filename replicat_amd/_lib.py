@@ -50,6 +50,8 @@ SIGNATURES = {
     'rc_chunker_overlap_cus': (_u32, [_p]),
     'rc_chunker_pipelined_calls': (_u64, [_p]),
     'rc_chunk_wait': (_int, [_p, _p]),
+    'rc_stream_create': (_int, [_int, ctypes.POINTER(_p)]),
+    'rc_stream_destroy': (None, [_p]),
     'rc_timing_enable': (_int, [_p, _int]),
     'rc_timing_read': (_int, [_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                               ctypes.POINTER(_u64)]),

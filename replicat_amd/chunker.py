@@ -177,6 +177,40 @@ class GpuChunker:
         return t.value, e.value, c.value, n.value
 
 
+class QueueStream:
+    """A HIP stream with a hardware queue of its own (rc_stream_create): kernels on it never
+    wait behind another stream's kernels on a shared queue, whatever GPU_MAX_HW_QUEUES is.  A
+    BLOCKING stream (CU-masked), so keep the legacy NULL stream out of the work it overlaps.
+    ``torch`` gives a torch.cuda.ExternalStream over it; close() (or exit) destroys it."""
+
+    def __init__(self, device=None):
+        if device is None:
+            device = _current_device()
+        h = ctypes.c_void_p()
+        check(lib().rc_stream_create(int(device), ctypes.byref(h)))
+        self.handle, self.device = h.value, int(device)
+        self._torch = None
+
+    @property
+    def torch(self):
+        if self._torch is None:
+            import torch
+            self._torch = torch.cuda.ExternalStream(self.handle, device=self.device)
+        return self._torch
+
+    def close(self):
+        h, self.handle = self.handle, None
+        self._torch = None
+        if h:
+            lib().rc_stream_destroy(h)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def tile_keys():
     return lib().rc_tile_keys()
 
@@ -227,5 +261,5 @@ def _current_device():
     return 0
 
 
-__all__ = ['GpuChunker', 'normalize_params', 'keys_needed', 'fill_splitmix', 'tables_key',
+__all__ = ['GpuChunker', 'QueueStream', 'normalize_params', 'keys_needed', 'fill_splitmix', 'tables_key',
            'MIN_LENGTH', 'MAX_LENGTH', '_lib']

@@ -935,6 +935,31 @@ int rc_chunk_device(rc_chunker *ch, uint64_t n, const uint8_t *const *d_streams,
                              (flags & RC_PIPELINE_END) != 0);
 }
 
+int rc_stream_create(int device, void **out_stream) {
+    if (!out_stream) return fail(RC_ERR_ARGUMENT, "null output stream");
+    *out_stream = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
+        return fail(RC_ERR_NO_DEVICE, "no HIP device %d", device);
+    DeviceGuard g(device);
+    int cus = 0;
+    HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+    std::vector<uint32_t> mask((cus + 31) / 32, 0u);
+    for (int i = 0; i < cus; ++i) mask[i / 32] |= 1u << (i % 32);
+    hipStream_t s = nullptr;
+    HIP_TRY(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
+    rc_track(s, [](void *h) { rc_stream_destroy(h); });
+    *out_stream = s;
+    return RC_OK;
+}
+
+void rc_stream_destroy(void *stream) {
+    if (!stream) return;
+    rc_untrack(stream);
+    (void)hipStreamSynchronize(static_cast<hipStream_t>(stream));
+    (void)hipStreamDestroy(static_cast<hipStream_t>(stream));
+}
+
 int rc_chunker_overlap(rc_chunker *ch, uint32_t reserve_cus) {
     if (!ch) return fail(RC_ERR_ARGUMENT, "null chunker");
     std::lock_guard<std::mutex> lock(ch->mu);

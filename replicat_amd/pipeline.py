@@ -61,7 +61,8 @@ from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 
-from .chunker import MAX_LENGTH, MIN_LENGTH, GpuChunker, _current_device, normalize_params
+from .chunker import (MAX_LENGTH, MIN_LENGTH, GpuChunker, QueueStream, _current_device,
+                      normalize_params)
 from .hashing import SLOT, GpuBlake2b, state_init
 from .snapshot import PIECE, PieceReader, file_parts, sort_files
 
@@ -292,7 +293,12 @@ class _Slot:
         self.d_count = torch.zeros(1, dtype=torch.int64, device=dev)
         self.d_digests = torch.zeros((max(prod.cut_cap, 1), SLOT), dtype=torch.uint8, device=dev)
         self.h_meta = torch.zeros(2, dtype=torch.int64, pin_memory=True)  # count, last cut end
-        self.stream = torch.cuda.Stream(device=dev)
+        # queues='own': a HIP stream with a hardware queue of its own (rc_stream_create), so this
+        # batch's ~55 ms digest chain never holds up the next batch's kernels on a shared queue
+        # (HIP's default GPU_MAX_HW_QUEUES=4 put a third slot stream behind the first, DESIGN.md
+        # §3b); 'shared': a torch stream on the process's shared queues
+        self.qs = QueueStream(prod.device) if prod.queues == 'own' else None
+        self.stream = self.qs.torch if self.qs is not None else torch.cuda.Stream(device=dev)
         self.ev_cut, self.ev_upd, self.ev_done = (torch.cuda.Event() for _ in range(3))
         if prod.encryption is not None:
             nb, total = prod.cipher.nonce_bytes, max(prod.cut_cap, 1)
@@ -309,7 +315,7 @@ class _Slot:
         self.reset(prod.head)
 
     def close(self):
-        for h in ('hasher', 'file_hasher', 'kdf_hasher', 'cipher'):
+        for h in ('hasher', 'file_hasher', 'kdf_hasher', 'cipher', 'qs'):
             obj = getattr(self, h, None)
             if obj is not None and hasattr(obj, 'close'):
                 obj.close()
@@ -333,7 +339,7 @@ class DeviceSnapshotProducer:
                  params: Optional[bytes] = None, digest_size: int = 64,
                  batch_bytes: int = DEFAULT_BATCH, device=None, keep_contents: bool = True,
                  encryption: Optional[ChunkEncryption] = None, file_digests: str = 'auto',
-                 slots: int = 2):
+                 slots: int = 2, queues: str = 'own'):
         import torch
         if device is None:
             device = _current_device()
@@ -342,6 +348,9 @@ class DeviceSnapshotProducer:
                              f'than the maximum one ({max_length})')
         if int(slots) < 2:
             raise ValueError('slots must be at least 2 (one batch filled while one is on the device)')
+        if queues not in ('own', 'shared'):
+            raise ValueError(f'queues must be own or shared, not {queues!r}')
+        self.queues = queues
         self.device = int(device)
         self.dev = torch.device('cuda', self.device)
         self.chunker = GpuChunker(min_length, max_length, normalize_params(params), device=self.device)
@@ -643,8 +652,13 @@ class _Run:
         count = int(s.h_meta[0])
         if count < 0:
             raise RuntimeError('cut capacity overflow')
-        ends = s.d_cuts[:count].cpu().numpy().view(np.uint64).astype(np.int64)
-        digs = s.d_digests[:count, :p.digest_size].cpu().numpy()
+        # every device read on the slot's own stream: the legacy NULL stream would wait for
+        # every blocking (own-queue) slot stream, i.e. for the later batches' digests too
+        with torch.cuda.stream(s.stream):
+            ends = s.d_cuts[:count].cpu().numpy().view(np.uint64).astype(np.int64)
+            digs = s.d_digests[:count, :p.digest_size].cpu().numpy()
+            fd = (s.file_digests[:, :p.digest_size].cpu().numpy()
+                  if s.file_digests is not None else None)
         enc = over = None
         if p.encryption is not None:
             over = p.cipher.nonce_bytes + 16
@@ -653,8 +667,7 @@ class _Run:
                 s.h_enc[:n_out].copy_(s.d_enc[:n_out], non_blocking=True)
             s.stream.synchronize()
             enc = s.h_enc[:n_out].numpy()
-        if s.file_digests is not None:
-            fd = s.file_digests[:, :p.digest_size].cpu().numpy()
+        if fd is not None:
             for j, (fi, fin) in enumerate(s.items):
                 if fin:
                     self.files[fi].digest = fd[j].tobytes()

@@ -10,7 +10,10 @@ distinct synthetic bytes (splitmix64, generated in HBM), queued round-robin on S
 and without the H2D upload of each batch from a pinned host buffer.  Digests of the first batch
 are checked against hashlib.
 
-    python scripts/digest_overlap_probe.py [--batches 8] [--slots 1,2,3,4]
+    python scripts/digest_overlap_probe.py [--batches 8] [--slots 1,2,3,4] [--queues torch|own]
+
+--queues own: each slot's stream has a hardware queue of its own (replicat_amd.chunker.QueueStream,
+rc_stream_create) instead of a torch stream on the process's shared GPU_MAX_HW_QUEUES queues.
 """
 import argparse
 import hashlib
@@ -26,7 +29,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from replicat_amd import synth  # noqa: E402
-from replicat_amd.chunker import GpuChunker, fill_splitmix  # noqa: E402
+from replicat_amd.chunker import GpuChunker, QueueStream, fill_splitmix  # noqa: E402
 from replicat_amd.hashing import SLOT, GpuBlake2b  # noqa: E402
 
 GIB = 1 << 30
@@ -38,6 +41,7 @@ def main():
     ap.add_argument('--batches', type=int, default=8)
     ap.add_argument('--batch-mib', type=int, default=1024)
     ap.add_argument('--slots', default='1,2,3,4')
+    ap.add_argument('--queues', choices=['torch', 'own'], default='torch')
     args = ap.parse_args()
     torch.cuda.set_device(0)
     size = args.batch_mib << 20
@@ -51,7 +55,9 @@ def main():
     ch = GpuChunker(MIN_LEN, MAX_LEN, b'\xff' * 16)
     cap, _ = ch.capacity([size])
     smax = max(int(s) for s in args.slots.split(','))
-    streams = [torch.cuda.Stream() for _ in range(smax)]
+    owned = [QueueStream() for _ in range(smax)] if args.queues == 'own' else []
+    streams = [q.torch for q in owned] if owned else [torch.cuda.Stream() for _ in range(smax)]
+    torch.cuda.set_stream(torch.cuda.Stream())  # keep the legacy NULL stream out of it
     hashers = [GpuBlake2b(length=64) for _ in range(smax)]
     cuts = [torch.zeros(cap, dtype=torch.int64, device='cuda') for _ in range(nb)]
     counts = [torch.zeros(1, dtype=torch.int64, device='cuda') for _ in range(nb)]
@@ -97,7 +103,9 @@ def main():
         for S in [int(s) for s in args.slots.split(',')]:
             run(S, upload)  # warm
             dt = min(run(S, upload) for _ in range(2))
-            print(json.dumps({'slots': S, 'upload_from_pinned': upload, 'batches': nb,
+            print(json.dumps({'slots': S, 'queues': args.queues,
+                              'GPU_MAX_HW_QUEUES': os.environ.get('GPU_MAX_HW_QUEUES'),
+                              'upload_from_pinned': upload, 'batches': nb,
                               'batch_bytes': size, 's': round(dt, 4),
                               'gib_s': round(nb * size / dt / GIB, 2),
                               'ms_per_batch': round(dt * 1e3 / nb, 2)}), flush=True)

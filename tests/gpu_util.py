@@ -14,7 +14,9 @@ def device_streams(sizes, seed=None, fill=None, datas=None, ids=None):
         t = torch.empty(max(int(n), 1) + 16, dtype=torch.uint8, device='cuda')
         if datas is not None:
             if n:
-                t[:n].copy_(torch.from_numpy(np.asarray(datas[i], dtype=np.uint8)))
+                # a writable copy: torch.from_numpy warns on (and may not own) read-only
+                # buffers such as np.frombuffer over bytes
+                t[:n].copy_(torch.from_numpy(np.array(datas[i], dtype=np.uint8, copy=True)))
         elif fill is not None:
             t.fill_(fill)
         else:

@@ -117,3 +117,30 @@ def test_producer_needs_two_slots(slots):
     before anything touches a device."""
     with pytest.raises(ValueError, match='slots'):
         pipeline.DeviceSnapshotProducer(slots=slots, device=0)
+
+
+def test_producer_queue_modes():
+    """queues='own' (the default: batch streams with hardware queues of their own) or 'shared'
+    (torch streams); anything else is refused before any device work."""
+    import inspect
+    sig = inspect.signature(pipeline.DeviceSnapshotProducer.__init__)
+    assert sig.parameters['queues'].default == 'own'
+    assert sig.parameters['slots'].default == 2
+    with pytest.raises(ValueError, match='queues'):
+        pipeline.DeviceSnapshotProducer(queues='many', device=0)
+
+
+def test_record_release_is_idempotent():
+    """stream() records hold a lease on their batch until release() (or garbage collection)."""
+    lease = pipeline._Lease()
+    recs = [pipeline.ChunkRecord(k + 1, k, k + 1, b'd', 0, memoryview(b'x'), lease)
+            for k in range(3)]
+    lease.take(3)
+    recs[0].release()
+    recs[0].release()
+    assert lease.n == 2 and recs[0].contents is None
+    del recs[1]
+    assert lease.n == 1
+    import threading
+    recs[-1].release()
+    assert lease.wait(threading.Event()) is True
