@@ -11,6 +11,7 @@ Streams follow replicat's piece framing (adapters.py:290-305): a stream of L byt
 piece starts at byte P is cut exactly as replicat's adapter loop cuts those pieces.
 """
 import ctypes
+import threading
 
 import numpy as np
 
@@ -181,7 +182,17 @@ class QueueStream:
     """A HIP stream with a hardware queue of its own (rc_stream_create): kernels on it never
     wait behind another stream's kernels on a shared queue, whatever GPU_MAX_HW_QUEUES is.  A
     BLOCKING stream (CU-masked), so keep the legacy NULL stream out of the work it overlaps.
-    ``torch`` gives a torch.cuda.ExternalStream over it; close() (or exit) destroys it."""
+    ``torch`` gives a torch.cuda.ExternalStream over it.
+
+    Lifetime: torch's caching allocator records events on the streams a tensor was used on
+    (``record_stream``) when it frees the tensor, possibly much later, so a stream torch has
+    seen must outlive every such tensor.  Take streams from the process-wide pool
+    (``QueueStream.acquire`` / ``release``): pooled streams are reused, never destroyed while
+    the process runs, and released by the library's exit hook after Python's own finalisation.
+    ``close()`` destroys a stream at once -- only for one torch never used."""
+
+    _pool = {}
+    _lock = threading.Lock()
 
     def __init__(self, device=None):
         if device is None:
@@ -190,6 +201,24 @@ class QueueStream:
         check(lib().rc_stream_create(int(device), ctypes.byref(h)))
         self.handle, self.device = h.value, int(device)
         self._torch = None
+
+    @classmethod
+    def acquire(cls, device=None):
+        """A pooled stream of `device` (a new one when none is free)."""
+        if device is None:
+            device = _current_device()
+        with cls._lock:
+            free = cls._pool.setdefault(int(device), [])
+            if free:
+                return free.pop()
+        return cls(device)
+
+    def release(self):
+        """Back to the pool (the caller's work on it may still be queued: the next user's work
+        follows it in stream order)."""
+        if self.handle:
+            with QueueStream._lock:
+                QueueStream._pool.setdefault(self.device, []).append(self)
 
     @property
     def torch(self):
@@ -203,12 +232,6 @@ class QueueStream:
         self._torch = None
         if h:
             lib().rc_stream_destroy(h)
-
-    def __del__(self):
-        try:
-            self.close()
-        except Exception:
-            pass
 
 
 def tile_keys():

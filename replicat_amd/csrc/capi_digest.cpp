@@ -159,7 +159,7 @@ int enqueue_items(rc_hasher *h, uint64_t n, const uint8_t *const *d_ptrs, const 
     for (uint64_t i = 0; i < n; ++i) msg_bytes += lens[i];
     const uint64_t lane_max = rc_b2_lane_max(msg_bytes, it[0].len, h->knobs[rc::knB2LaneMax]);
     if (rc_b2_launch_items(static_cast<const B2Item *>(w->d_stage.p), n, h->digest_size, d_out,
-                           lane_max, rc_b2_lane_only(lane_max, it[0].len, h->knobs[rc::knB2LaneOnly]),
+                           lane_max, rc_b2_lane_only(lane_max, it[0].len, h->knobs[rc::knB2LaneOnly] == 1),
                            st))
         return rc_fail(RC_ERR_HIP, "%s", rc_b2_launch_error());
     if (int rc = timing_end(h, st, ev)) return rc;
@@ -228,7 +228,7 @@ int rc_hasher_enqueue_chunks(rc_hasher *h, uint64_t n, const uint8_t *const *d_p
     const uint64_t lane_max = rc_b2_lane_max(bytes, longest, h->knobs[rc::knB2LaneMax]);
     if (rc_b2_launch_chunks(n, d, d + n, d_cuts, d_counts, chunk_off, hist,
                             static_cast<B2Item *>(w->d_items.p), total_cap, h->digest_size, d_out,
-                            lane_max, rc_b2_lane_only(lane_max, longest, h->knobs[rc::knB2LaneOnly]),
+                            lane_max, rc_b2_lane_only(lane_max, longest, h->knobs[rc::knB2LaneOnly] == 1),
                             st))
         return rc_fail(RC_ERR_HIP, "%s", rc_b2_launch_error());
     if (int rc = timing_end(h, st, ev)) return rc;

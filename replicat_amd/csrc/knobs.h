@@ -80,8 +80,9 @@ inline constexpr KnobSpec kKnobTable[kKnobCount] = {
      "0: no boundary repair in the merge kernel (a miss walks the stream)"},
     {"RC_B2_LANE_MAX", -1, -1, int64_t(1) << 62, nullptr,
      "BLAKE2b: longest message hashed by one lane (-1: the throughput rule, 0: quads only)"},
-    {"RC_B2_LANE_ONLY", 0, 0, 1, "auto|0",
-     "BLAKE2b: 0 never uses the lane-only kernel (the fused kernel's lane role instead)"},
+    {"RC_B2_LANE_ONLY", 0, 0, 2, "auto|0|1",
+     "BLAKE2b: 0 never uses the lane-only kernel (the fused kernel's lane role instead); "
+     "auto and 1 use it when every message fits a lane"},
     {"RC_PROBE_BLOCK", 0, 0, int64_t(1) << 20, nullptr,
      "read probe: interleaved static runs of this many tiles (0: the tile kernel's schedule)"},
     {"RC_GCM_DEBUG", 0, 0, 1, "0|1",

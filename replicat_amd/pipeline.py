@@ -297,7 +297,7 @@ class _Slot:
         # batch's ~55 ms digest chain never holds up the next batch's kernels on a shared queue
         # (HIP's default GPU_MAX_HW_QUEUES=4 put a third slot stream behind the first, DESIGN.md
         # §3b); 'shared': a torch stream on the process's shared queues
-        self.qs = QueueStream(prod.device) if prod.queues == 'own' else None
+        self.qs = QueueStream.acquire(prod.device) if prod.queues == 'own' else None
         self.stream = self.qs.torch if self.qs is not None else torch.cuda.Stream(device=dev)
         self.ev_cut, self.ev_upd, self.ev_done = (torch.cuda.Event() for _ in range(3))
         if prod.encryption is not None:
@@ -315,10 +315,14 @@ class _Slot:
         self.reset(prod.head)
 
     def close(self):
-        for h in ('hasher', 'file_hasher', 'kdf_hasher', 'cipher', 'qs'):
+        for h in ('hasher', 'file_hasher', 'kdf_hasher', 'cipher'):
             obj = getattr(self, h, None)
             if obj is not None and hasattr(obj, 'close'):
                 obj.close()
+        qs, self.qs = getattr(self, 'qs', None), None
+        if qs is not None:
+            self.stream.synchronize()
+            qs.release()  # pooled, never destroyed: torch may still record events on it
 
     def reset(self, head):
         self.off = head          # host offset of the batch's first byte

@@ -55,7 +55,7 @@ def main():
     ch = GpuChunker(MIN_LEN, MAX_LEN, b'\xff' * 16)
     cap, _ = ch.capacity([size])
     smax = max(int(s) for s in args.slots.split(','))
-    owned = [QueueStream() for _ in range(smax)] if args.queues == 'own' else []
+    owned = [QueueStream.acquire() for _ in range(smax)] if args.queues == 'own' else []
     streams = [q.torch for q in owned] if owned else [torch.cuda.Stream() for _ in range(smax)]
     torch.cuda.set_stream(torch.cuda.Stream())  # keep the legacy NULL stream out of it
     hashers = [GpuBlake2b(length=64) for _ in range(smax)]
