@@ -99,15 +99,19 @@ class _Lease:
             if self.n == 0:
                 self.cv.notify_all()
 
-    def wait(self, abort, warn_after=60.0):
-        """Until every record is released; False if `abort` (an Event) was set first.  A
-        consumer that keeps records without releasing them stalls the producer: say so once."""
+    def wait(self, abort, timeout=None, warn_after=60.0):
+        """Until every record is released; False if `abort` (an Event) was set first,
+        TimeoutError after `timeout` seconds.  A consumer that keeps records without releasing
+        them stalls the producer: say so once."""
         t0, warned = time.monotonic(), False
         with self.cv:
             while self.n:
                 if abort.is_set():
                     return False
                 self.cv.wait(0.05)
+                if timeout is not None and time.monotonic() - t0 > timeout:
+                    raise TimeoutError(f'{self.n} ChunkRecord(s) of a batch unreleased for '
+                                       f'{timeout} s: release() each record when done with it')
                 if not warned and time.monotonic() - t0 > warn_after:
                     warned = True
                     import warnings
@@ -457,13 +461,19 @@ class DeviceSnapshotProducer:
                             abort=threading.Event())
         return SnapshotStream(files=files, chunks=run.chunks, chunks_table=run.table)
 
-    def stream(self, paths: Sequence[os.PathLike], read=None) -> 'ChunkStream':
+    def stream(self, paths: Sequence[os.PathLike], read=None,
+               stall_timeout: Optional[float] = None) -> 'ChunkStream':
         """The chunks as they are produced (a ``ChunkStream``: iterate it for ``ChunkRecord``s
         whose ``contents`` view the pinned batches -- release() each when done), produced on a
-        thread of its own like replicat's chunk-producer thread (repository.py:1358,1556)."""
-        return ChunkStream(self, paths, read)
+        thread of its own like replicat's chunk-producer thread (repository.py:1358,1556).
+        The records must be released by someone other than the loop that waits for the next
+        one (upload workers, as replicat's _worker coroutines), or right away: a loop that
+        holds more records than the other slots can carry waits for itself.  stall_timeout:
+        seconds the producer waits for a batch's records before it fails the stream with a
+        TimeoutError (None: it waits, and warns after a minute)."""
+        return ChunkStream(self, paths, read, stall_timeout)
 
-    def _produce(self, paths, read, files, zero_copy, sink, abort):
+    def _produce(self, paths, read, files, zero_copy, sink, abort, stall_timeout=None):
         """Batch k + 1 is read from the files while the device cuts and digests batch k, and
         batch k's records are built while the device works on batch k + 1.  The uncut tail of
         batch k (known once its cut chain is done, long before its digests) is copied to the
@@ -498,7 +508,7 @@ class DeviceSnapshotProducer:
                     prof['collect_join'] += clock() - t
                 # and every stream() record viewing its bytes released (also across runs)
                 t = clock()
-                if not s.lease.wait(abort):
+                if not s.lease.wait(abort, stall_timeout):
                     raise _Aborted()
                 prof['release_wait'] += clock() - t
                 s.reset(self.head)
@@ -736,7 +746,7 @@ class ChunkStream:
 
     _END = object()
 
-    def __init__(self, prod, paths, read=None):
+    def __init__(self, prod, paths, read=None, stall_timeout=None):
         import queue
         self.files: List[FileRecord] = []
         self._q = queue.Queue()
@@ -747,7 +757,8 @@ class ChunkStream:
         def work():
             try:
                 self._run = prod._produce(paths, read, self.files, zero_copy=True,
-                                          sink=self._q.put, abort=self._abort)
+                                          sink=self._q.put, abort=self._abort,
+                                          stall_timeout=stall_timeout)
                 self._q.put(self._END)
             except _Aborted:
                 self._q.put(self._END)

@@ -200,15 +200,15 @@ def test_close_and_context_manager(tmp_path):
 
 # ------------------------------------------------------------- stream(): zero-copy records
 
-def _streamed(prod, paths, hold=0, workers=0):
-    """Consume prod.stream(paths) the way replicat's upload workers take _SnapshotChunks
-    (repository.py:1492, 1507-1554): each record's contents are checked against its digest at
-    the moment it is 'uploaded', then released.  hold: records kept unreleased in a FIFO (an
-    upload queue) before the oldest is handled; workers > 0: handled on that many threads."""
-    import collections
-    import concurrent.futures as cf
-    out, held, bad = [], collections.deque(), []
-
+def _streamed(prod, paths, queue_size=0, workers=0):
+    """Consume prod.stream(paths) the way replicat's snapshot loop does (repository.py:1355,
+    1492, 1507-1554): workers=0 -- each record 'uploaded' (its contents checked against its
+    digest) and released at once; otherwise the records go through a bounded queue of
+    queue_size to `workers` upload threads that release them after their upload, out of order
+    and later than the producer moves on."""
+    import queue as Q
+    import threading
+    out, bad, lock = {}, [], threading.Lock()
     plain = prod.encryption is None  # encrypted contents are nonce || C || T
 
     def upload(rec):
@@ -216,47 +216,56 @@ def _streamed(prod, paths, hold=0, workers=0):
         if plain and hashlib.blake2b(data).digest() != rec.digest:
             bad.append(rec.counter)
         rec.release()
-        return rec.counter, data
+        with lock:
+            out[rec.counter] = data
 
-    pool = cf.ThreadPoolExecutor(workers) if workers else None
-    futs = []
-    with prod.stream(paths) as st:
-        for rec in st:
-            assert isinstance(rec.contents, memoryview) and rec.contents.readonly
-            held.append(rec)
-            while len(held) > hold:
-                r = held.popleft()
-                if pool:
-                    futs.append(pool.submit(upload, r))
+    q = Q.Queue(maxsize=queue_size) if workers else None
+
+    def worker():
+        while True:
+            rec = q.get()
+            if rec is None:
+                return
+            upload(rec)
+
+    threads = [threading.Thread(target=worker) for _ in range(workers)]
+    for t in threads:
+        t.start()
+    try:
+        with prod.stream(paths, stall_timeout=60) as st:
+            for rec in st:
+                assert isinstance(rec.contents, memoryview) and rec.contents.readonly
+                if q is None:
+                    upload(rec)
                 else:
-                    out.append(upload(r))
-        while held:
-            out.append(upload(held.popleft()))
-        res = st.snapshot()
-    if pool:
-        out += [f.result() for f in futs]
-        pool.shutdown()
+                    q.put(rec)
+                del rec
+            res = st.snapshot()
+    finally:
+        for _ in threads:
+            q.put(None)
+        for t in threads:
+            t.join()
     assert not bad, bad[:5]
-    data = dict(out)
     for c in res.chunks:  # the run's records carry no contents: give them the uploaded bytes
         assert c.contents is None
-        c.contents = data[c.counter]
+        c.contents = out[c.counter]
     return res
 
 
 @pytest.mark.parametrize('name', sorted(SNAPS))
-@pytest.mark.parametrize('hold,workers', [(0, 0), (40, 0), (8, 4)])
-def test_stream_reference_snapshots(tmp_path, name, hold, workers):
+@pytest.mark.parametrize('queue_size,workers', [(0, 0), (50, 5), (3, 2)])
+def test_stream_reference_snapshots(tmp_path, name, queue_size, workers):
     """stream() gives the reference's chunks, digests and file ranges with views into the
-    pinned batches; records held across batch boundaries (hold) or released on other threads
-    (workers) never see a refilled buffer."""
+    pinned batches; records released late and out of order by upload workers (replicat's
+    queue of concurrent * 10 and 5 workers) never see a refilled buffer."""
     s = SNAPS[name]
     files_data = file_sets()[name]
     paths = write(tmp_path, files_data)
     params = None if s['params'] is None else bytes.fromhex(s['params'])
     prod = DeviceSnapshotProducer(min_length=s['min'], max_length=s['max'], params=params,
                                   batch_bytes=1 << 20)
-    res = _streamed(prod, paths, hold, workers)
+    res = _streamed(prod, paths, queue_size, workers)
     check_stream(res, files_data, s['lengths'])
     # the same producer again, now through run(): the same stream
     again = prod.run(paths)
@@ -291,7 +300,7 @@ def test_stream_encrypted_and_abandoned(oracle, tmp_path):
             if n == 40:
                 break  # abandoned: the producer thread stops at its next batch
     assert n == 40
-    res = _streamed(prod, paths, hold=5)
+    res = _streamed(prod, paths, queue_size=10, workers=3)
     assert res.chunks[-1].stream_end == len(stream)
     for c in res.chunks:
         blob = c.contents
