@@ -895,28 +895,19 @@ int rc_chunk_device(rc_chunker *ch, uint64_t n, const uint8_t *const *d_streams,
     if (!d_cuts || !d_counts) return fail(RC_ERR_ARGUMENT, "null output arrays");
     const bool open = (flags & RC_OPEN) != 0;
     if (int rc = validate_streams(n, d_streams, lens, open ? nullptr : last_piece, true)) return rc;
-    // Two kinds of call run a pipelined request in sequence on the caller's stream -- a legal
-    // schedule of the flag (inputs and outputs in that stream's order) -- because the overlap
-    // cost more than it hid (scripts/overlap_ab.py, profiles/r03/overlap/):
-    // * small windows (group records, lane / quad chains: config 3 iii): their chain takes
-    //   2.8 ms on 32 CUs and their VALU-heavier tile kernel lost 3 % on 224 CUs;
-    // * launches on the tile kernel's static schedule (fewer than 128 tiles per wave: the
-    //   harness's one 5.12 GB stream): on 224 CUs the static shares grow, 0.85 -> 0.92 ms.
-    // RC_PIPE_ALL=1 pipelines every call (tests, measurements).
+    // Small-window chunkers (group records, lane / quad chains: config 3 iii) run a pipelined
+    // request in sequence on the caller's stream -- a legal schedule of the flag (inputs and
+    // outputs in that stream's order): their quad chain takes 2.8 ms on 32 CUs and their
+    // VALU-heavier tile kernel lost 3 % on 224 CUs (scripts/overlap_ab.py, profiles/r03/overlap/).
+    // Round 4 re-measured launches on the static schedule (the harness: one 5.12 GB stream,
+    // 76 tiles per wave), which round 3 also ran in sequence: on one allocation the tile kernel
+    // takes 0.833 ms on 224 CUs as on 256, and pipelined steps 0.876 ms against 0.950 in sequence
+    // (profiles/r04/harness/harness_sched.log), so they pipeline now.  RC_PIPE_ALL=1 pipelines
+    // every call (tests, measurements).
     std::lock_guard<std::mutex> lock(ch->mu);
-    DeviceGuard g(ch->device);  // rc_tile_dynamic counts the CUs of the current device
+    DeviceGuard g(ch->device);
     const bool all = ch->knobs[knPipeAll] != 0;
     bool pipelined = (flags & RC_PIPELINED) != 0 && (all || !ch->groups);
-    if (pipelined && !all) {
-        uint64_t tiles = 0;
-        for (uint64_t i = 0; i < n; ++i) {
-            const uint64_t P = open ? lens[i] : last_piece ? last_piece[i] : 0;
-            const uint64_t jn = rc_keys_needed(ch->max_length, lens[i], P);
-            tiles += jn ? jn / kTileKeys + 1 : 0;
-        }
-        pipelined = rc_tile_dynamic(tiles, 0, ch->sched) != 0;
-    }
-
     // no CU-masked streams on this device / runtime: the request runs in sequence (the call
     // stays correct; rc_chunker_overlap reports the error, rc_chunker_overlap_cus stays 0)
     if (pipelined && !ch->overlap_failed && setup_overlap(ch) != 0) {

@@ -148,9 +148,6 @@ int rc_launch_tiles(const rc::KeyTables *d_tables, rc::StreamDesc desc, uint64_t
                     void *mid_event, uint32_t cus, void *edge_stream, void *tiled,
                     rc::TileSched sched);
 uint64_t rc_tie_list_words(uint64_t n_tiles);
-// 1 if a tile launch over n_tiles on `cus` CUs of the CURRENT device (0 = all) hands out dynamic
-// units, 0 if it is fully static (fewer than sched.dyn_min tiles per wave)
-int rc_tile_dynamic(uint64_t n_tiles, uint32_t cus, rc::TileSched sched);
 // join: RC_JOIN_* bits -- how multi-segment streams are spliced
 enum : uint32_t { RC_JOIN_WALK_ONLY = 1, RC_JOIN_REPAIR = 2 };
 int rc_launch_chain(const rc::KeyTables *d_tables, rc::StreamDesc desc, uint64_t n_streams,

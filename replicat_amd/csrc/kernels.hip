@@ -2860,13 +2860,6 @@ uint64_t rc_tie_list_words(uint64_t n_tiles) {
     return 2 * n_tiles + n_tiles / kDynChunkMin + 64;
 }
 
-int rc_tile_dynamic(uint64_t n_tiles, uint32_t cus, TileSched sched) {
-    if (n_tiles == 0) return 0;
-    const TileUnits U = tile_units(n_tiles, (uint64_t)(cus ? cus : (uint32_t)cu_count()) * (1024 / kWaveSize),
-                                   sched);
-    return U.n_units > U.nw;
-}
-
 int rc_launch_chain(const KeyTables *d_tables, StreamDesc desc, uint64_t n_streams,
                     ChainParams prm, uint64_t n_segs, const TileRecord *d_records,
                     uint64_t *d_cuts, int64_t *d_counts, uint64_t *d_scratch,

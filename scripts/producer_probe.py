@@ -72,6 +72,56 @@ for name, kw in variants:
     if name == 'plain':
         plain = res
 
+
+# stream(): zero-copy records (views into the pinned batches), consumed as replicat's upload
+# workers take _SnapshotChunks (repository.py:1355,1492,1507-1554): 'release' hands each record
+# back at once (the producer's own rate); 'workers' puts them on a queue of concurrent * 10 = 50
+# for 5 threads that touch every byte (a checksum pass standing in for the upload) and release
+def consume(prod, workers):
+    import queue
+    import threading
+    import zlib
+    q = queue.Queue(maxsize=50)
+    n = [0]
+
+    def work():
+        while (r := q.get()) is not None:
+            zlib.adler32(r.contents)
+            r.release()
+
+    ts = [threading.Thread(target=work) for _ in range(workers)]
+    for t in ts:
+        t.start()
+    with prod.stream(paths) as st:
+        for r in st:
+            n[0] += 1
+            if workers:
+                q.put(r)
+            else:
+                r.release()
+            del r
+        snap = st.snapshot()
+    for _ in ts:
+        q.put(None)
+    for t in ts:
+        t.join()
+    return snap
+
+
+if hasattr(DeviceSnapshotProducer, 'stream'):
+    for name, workers, kw in (('stream_release', 0, {}), ('stream_5_workers', 5, {}),
+                              ('stream_release_encrypted', 0, {'encryption': enc})):
+        prod = DeviceSnapshotProducer(min_length=MIN, max_length=MAX, **kw)
+        dt, snap = timed(lambda: consume(prod, workers))
+        if not kw:
+            assert [c.stream_end for c in snap.chunks] == [c.stream_end for c in plain.chunks]
+            assert [c.digest for c in snap.chunks] == [c.digest for c in plain.chunks]
+        print(json.dumps({'variant': name, 'bytes': total, 'files': nfiles,
+                          'chunks': len(snap.chunks), 's': round(dt, 4),
+                          'gib_s': round(total / dt / GIB, 3),
+                          'phases_s': {k: round(v, 4) for k, v in prod.profile.items()}}),
+              flush=True)
+
 # CPU baseline: the oracle's chunker + hashlib over the same framed stream (one core)
 def cpu_leg():
     pieces = list(snapshot.stream_pieces(snapshot.sort_files(paths)))

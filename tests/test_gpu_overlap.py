@@ -245,41 +245,34 @@ def test_pipeline_end_orders_shared_outputs(pipe_all):
         assert _ends(cuts, counts, caps) == exp[plan[k - 1][0]], plan[:k]
 
 
-@pytest.mark.parametrize('downgrade', [False, True])
-def test_sequential_after_pipelined_shares_outputs(downgrade, monkeypatch):
+@pytest.mark.parametrize('end', [False, True])
+def test_sequential_after_pipelined_shares_outputs(end):
     """a call in sequence right after pipelined ones on the same chunker, into the
     SAME cut and count arrays, must end with its own cuts -- the pipelined calls' chains may
-    still run on the reserved CUs' stream when the later call's chain starts on the caller's
-    stream.  downgrade: the later call asks for RC_PIPELINED and the library runs it in sequence
-    (a small batch after 8 GiB pipelined ones); otherwise it is a plain sequential call."""
-    if not downgrade:
-        monkeypatch.setenv('RC_PIPE_ALL', '1')  # read at creation: small batches pipeline too
+    still run on the reserved CUs' stream (end: on the every-CU stream of RC_PIPELINE_END) when
+    the later call's chain starts on the caller's stream."""
     ch = GpuChunker(MIN_LENGTH, MAX_LENGTH, b'\xff' * 16)
-    size = 16 * MIB
-    # 160 x 64 MiB: enough tiles per wave for the dynamic schedule, so the A calls pipeline
-    na, sa = (160, 64 * MIB) if downgrade else (24, size)
-    nb = 24
-    a = torch.empty(na * sa + 64, dtype=torch.uint8, device='cuda')
+    size, na, nb = 16 * MIB, 48, 24
+    a = torch.empty(na * size + 64, dtype=torch.uint8, device='cuda')
     b = torch.empty(nb * size + 64, dtype=torch.uint8, device='cuda')
-    fill_splitmix_streams(a.data_ptr(), na, sa, sa, synth.DEFAULT_SEED, 700, 1, _hs())
+    fill_splitmix_streams(a.data_ptr(), na, size, size, synth.DEFAULT_SEED, 700, 1, _hs())
     fill_splitmix_streams(b.data_ptr(), nb, size, size, synth.DEFAULT_SEED, 3000, 1, _hs())
     seq = GpuChunker(MIN_LENGTH, MAX_LENGTH, b'\xff' * 16)
     exp_b = chunk_device(seq, [b[i * size:(i + 1) * size] for i in range(nb)], [size] * nb)
-    total, caps = ch.capacity([sa] * na)
+    total, caps = ch.capacity([size] * na)
     _, caps_b = ch.capacity([size] * nb)
     cuts = torch.zeros(total, dtype=torch.int64, device='cuda')
     counts = torch.zeros(na, dtype=torch.int64, device='cuda')
-    pa = np.arange(na, dtype=np.uint64) * sa + a.data_ptr()
+    pa = np.arange(na, dtype=np.uint64) * size + a.data_ptr()
     pb = np.arange(nb, dtype=np.uint64) * size + b.data_ptr()
     for rnd in range(3):
-        for _ in range(2):
-            ch.chunk_device(pa, [sa] * na, None, cuts.data_ptr(), counts.data_ptr(), _hs(),
-                            pipelined=True)
+        for k in range(2):
+            ch.chunk_device(pa, [size] * na, None, cuts.data_ptr(), counts.data_ptr(), _hs(),
+                            pipelined=True, end=end and k == 1)
         before = ch.pipelined_calls()
-        ch.chunk_device(pb, [size] * nb, None, cuts.data_ptr(), counts.data_ptr(), _hs(),
-                        pipelined=downgrade)
+        assert before == 2 * (rnd + 1)  # the A calls were pipelined
+        ch.chunk_device(pb, [size] * nb, None, cuts.data_ptr(), counts.data_ptr(), _hs())
         assert ch.pipelined_calls() == before  # the B call ran in sequence
-        assert before == 2 * (rnd + 1)         # the A calls were pipelined
         ch.wait(_hs())
         got = _ends(cuts[:int(caps_b.sum())], counts[:nb], caps_b)
         assert got == exp_b, rnd
