@@ -117,6 +117,7 @@ struct TileSched {
     uint32_t permille = 100;
     uint32_t chunk = 12;
     uint32_t dyn_min = 128;
+    uint32_t guided = 0;  // shrinking units at the end of the dynamic tiles (RC_TILE_GUIDED)
 };
 
 // splitmix64 finaliser (replicat_amd/synth.py)
@@ -148,6 +149,7 @@ int rc_launch_tiles(const rc::KeyTables *d_tables, rc::StreamDesc desc, uint64_t
                     void *mid_event, uint32_t cus, void *edge_stream, void *tiled,
                     rc::TileSched sched);
 uint64_t rc_tie_list_words(uint64_t n_tiles);
+// (exported for tests: include/replicat_chunker.h rc_tile_schedule)
 // join: RC_JOIN_* bits -- how multi-segment streams are spliced
 enum : uint32_t { RC_JOIN_WALK_ONLY = 1, RC_JOIN_REPAIR = 2 };
 int rc_launch_chain(const rc::KeyTables *d_tables, rc::StreamDesc desc, uint64_t n_streams,
