@@ -211,11 +211,10 @@ uint64_t rc_tile_keys(void);
 
 /* Host-only inspection of the tile kernel's work units (tests; no device needed): the units a
  * launch over n_tiles tiles by `waves` waves hands out under the schedule knobs (RC_TILE_STATIC,
- * RC_TILE_CHUNK, RC_TILE_DYN_MIN, RC_TILE_GUIDED): unit u covers tiles
- * [ranges[2u], ranges[2u + 1]); *n_units receives the count, at most cap are written. */
+ * RC_TILE_CHUNK, RC_TILE_DYN_MIN): unit u covers tiles [ranges[2u], ranges[2u + 1]); *n_units
+ * receives the count, at most cap are written. */
 int rc_tile_schedule(uint64_t n_tiles, uint32_t waves, uint32_t permille, uint32_t chunk,
-                     uint32_t dyn_min, uint32_t guided, uint32_t *ranges, uint64_t cap,
-                     uint64_t *n_units);
+                     uint32_t dyn_min, uint32_t *ranges, uint64_t cap, uint64_t *n_units);
 
 /* Host-only check of the table construction (no device needed): out[i] = key of data word
  * ds[i] under the 16-byte key, evaluated from the same byte tables the kernels use, and

@@ -68,7 +68,7 @@ SIGNATURES = {
     'rc_tile_records': (_int, [_p, _u64, _p, _p, _p, _p, _p, _p, _p, _u64, ctypes.POINTER(_u64)]),
     'rc_group_hot_threshold': (_u32, [_p]),
     'rc_tile_keys': (_u64, []),
-    'rc_tile_schedule': (_int, [_u64, _u32, _u32, _u32, _u32, _u32, _p, _u64, ctypes.POINTER(_u64)]),
+    'rc_tile_schedule': (_int, [_u64, _u32, _u32, _u32, _u32, _p, _u64, ctypes.POINTER(_u64)]),
     # replicat_digest.h
     'rc_blake2b_create': (_int, [_u32, _int, ctypes.POINTER(_p)]),
     'rc_blake2b_destroy': (None, [_p]),

@@ -724,7 +724,6 @@ int rc_chunker_create(uint64_t min_length, uint64_t max_length, const uint8_t *k
     ch->sched.permille = (uint32_t)knobs[knTileStatic];
     ch->sched.chunk = (uint32_t)knobs[knTileChunk];
     ch->sched.dyn_min = (uint32_t)knobs[knTileDynMin];
-    ch->sched.guided = (uint32_t)knobs[knTileGuided];
     ch->k0 = k0;
     ch->k1 = k1;
     ch->device = device;

@@ -117,7 +117,6 @@ struct TileSched {
     uint32_t permille = 100;
     uint32_t chunk = 12;
     uint32_t dyn_min = 128;
-    uint32_t guided = 0;  // shrinking units at the end of the dynamic tiles (RC_TILE_GUIDED)
 };
 
 // splitmix64 finaliser (replicat_amd/synth.py)

@@ -511,33 +511,15 @@ __device__ __forceinline__ GroupRecord tile_groups(const uint32_t (&gpk)[(G + 1)
 // Static share 25 % and 32-tile units: 10-11 % faster on configs 2, 3 (iii) and 4 than fully
 // static on the same allocation; late in round 3, 10 % and 12-tile units took ~4 % more off
 // (tile_units).
-//
-// Round 4, the guided tail (TileSched.guided, RC_TILE_GUIDED): the dynamic tiles are handed out
-// in phases of shrinking units -- the bulk in `chunk`-tile units, then two units per wave of
-// chunk / 2, chunk / 4 and 2 tiles -- so the launch's last units, whose length is the spread of
-// the waves' finishing times, are 2 tiles instead of 12 for ~6 more grabs per wave.
 struct TileUnits {  // tile indices fit 32 bits (the tie lists store them as u32)
-    uint32_t n_tiles, nw, s0, dyn0, chunk, n_units;
-    // the guided tail (units from tail_u on; n_units when there is none): two units per wave of
-    // chunk / 2, then of each halving while above 2 tiles, then 2-tile units to the end
-    uint32_t tail_u;
+    uint32_t n_tiles, nw, s0, chunk, dyn0, n_units;
     __device__ __host__ void range(uint32_t u, uint32_t &b, uint32_t &e) const {
         if (u < nw) {
             b = u * s0;
             e = b + s0;
-        } else if (u < tail_u) {
+        } else {
             b = dyn0 + (u - nw) * chunk;
             e = b + chunk;
-        } else {
-            uint32_t off = u - tail_u, t = dyn0 + (tail_u - nw) * chunk;
-            uint32_t c = chunk / 2 < 2u ? 2u : chunk / 2;
-            while (c > 2u && off >= 2 * nw) {
-                off -= 2 * nw;
-                t += 2 * nw * c;
-                c = c / 2 < 2u ? 2u : c / 2;
-            }
-            b = t + off * c;
-            e = b + c;
         }
         if (b > n_tiles) b = n_tiles;
         if (e > n_tiles) e = n_tiles;
@@ -559,7 +541,7 @@ struct TileUnits {  // tile indices fit 32 bits (the tie lists store them as u32
 // 9.68 sequential, 3 iii 9.98 -> 9.94; 0 %: 9.72; profiles/r03/sched_static/): ~290 k grabs.
 constexpr uint64_t kDynChunkMin = 2;    // units of at least 2 tiles
 __host__ inline TileUnits tile_units(uint64_t n_tiles, uint64_t nw, TileSched sched) {
-    TileUnits U = {};
+    TileUnits U;
     U.n_tiles = (uint32_t)n_tiles;
     U.nw = (uint32_t)nw;
     uint64_t permille = sched.permille, chunk = sched.chunk, dyn_min = sched.dyn_min;
@@ -567,9 +549,9 @@ __host__ inline TileUnits tile_units(uint64_t n_tiles, uint64_t nw, TileSched sc
     if (chunk < kDynChunkMin) chunk = kDynChunkMin;
     if (n_tiles < dyn_min * nw || permille == 1000) {  // fully static
         U.s0 = (uint32_t)((n_tiles + nw - 1) / nw);
-        U.dyn0 = (uint32_t)n_tiles;
         U.chunk = 1;
-        U.n_units = U.tail_u = (uint32_t)nw;
+        U.dyn0 = (uint32_t)n_tiles;
+        U.n_units = (uint32_t)nw;
         return U;
     }
     U.s0 = (uint32_t)(n_tiles * permille / 1000 / nw);
@@ -578,24 +560,7 @@ __host__ inline TileUnits tile_units(uint64_t n_tiles, uint64_t nw, TileSched sc
     if (chunk > fit) chunk = fit > kDynChunkMin ? fit : kDynChunkMin;
     U.chunk = (uint32_t)chunk;
     U.dyn0 = (uint32_t)(nw * U.s0);
-    // the guided tail: two units per wave of chunk / 2, chunk / 4, ... while above 2 tiles, then
-    // 2-tile units (at least two per wave), taken from the end of the dynamic tiles
-    U.n_units = (uint32_t)(nw + (dyn + chunk - 1) / chunk);
-    U.tail_u = U.n_units;
-    if (sched.guided && chunk > kDynChunkMin) {
-        uint64_t mid_units = 0, mid_tiles = 0;
-        for (uint64_t c = chunk / 2 < 2 ? 2 : chunk / 2; c > 2; c = c / 2 < 2 ? 2 : c / 2) {
-            mid_units += 2 * nw;
-            mid_tiles += 2 * nw * c;
-        }
-        const uint64_t tail_min = mid_tiles + 2 * nw * kDynChunkMin;
-        if (dyn >= tail_min + 4 * nw * chunk) {
-            const uint64_t bulk_units = (dyn - tail_min) / chunk;
-            const uint64_t last = dyn - bulk_units * chunk - mid_tiles;  // in 2-tile units
-            U.tail_u = (uint32_t)(nw + bulk_units);
-            U.n_units = (uint32_t)(U.tail_u + mid_units + (last + 1) / 2);
-        }
-    }
+    U.n_units = (uint32_t)(nw + (n_tiles - U.dyn0 + chunk - 1) / chunk);
     return U;
 }
 
@@ -2890,14 +2855,12 @@ int rc_launch_tiles(const KeyTables *d_tables, StreamDesc desc, uint64_t n_strea
 }
 
 int rc_tile_schedule(uint64_t n_tiles, uint32_t waves, uint32_t permille, uint32_t chunk,
-                     uint32_t dyn_min, uint32_t guided, uint32_t *ranges, uint64_t cap,
-                     uint64_t *n_units) {
+                     uint32_t dyn_min, uint32_t *ranges, uint64_t cap, uint64_t *n_units) {
     if (!n_units || waves == 0 || n_tiles >= (1ull << 32)) return 1;
     TileSched sched;
     sched.permille = permille;
     sched.chunk = chunk;
     sched.dyn_min = dyn_min;
-    sched.guided = guided;
     const TileUnits U = tile_units(n_tiles, waves, sched);
     *n_units = U.n_units;
     for (uint32_t u = 0; u < U.n_units && u < cap && ranges; ++u) U.range(u, ranges[2 * u], ranges[2 * u + 1]);

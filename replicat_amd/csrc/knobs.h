@@ -29,7 +29,6 @@ enum Knob : int {
     knTileStatic,     // RC_TILE_STATIC
     knTileChunk,      // RC_TILE_CHUNK
     knTileDynMin,     // RC_TILE_DYN_MIN
-    knTileGuided,     // RC_TILE_GUIDED
     knJoinWalk,       // RC_JOIN_WALK
     knRepair,         // RC_REPAIR
     knB2LaneMax,      // RC_B2_LANE_MAX
@@ -75,8 +74,6 @@ inline constexpr KnobSpec kKnobTable[kKnobCount] = {
      "tiles per dynamic unit of the tile kernel"},
     {"RC_TILE_DYN_MIN", 128, 0, int64_t(1) << 20, nullptr,
      "tiles per wave from which a launch hands out dynamic units"},
-    {"RC_TILE_GUIDED", 0, 0, 1, "0|1",
-     "1: the dynamic units shrink at the end of a launch (two per wave of chunk/2, chunk/4, 2)"},
     {"RC_JOIN_WALK", 0, 0, 1, "0|1",
      "1: every multi-segment stream through the sequential join (comparison)"},
     {"RC_REPAIR", 1, 0, 1, "0|1",

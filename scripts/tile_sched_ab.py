@@ -10,7 +10,7 @@ time per setting is printed.
     python scripts/tile_sched_ab.py 2 6 1000:32 750:32 500:16 500:64
 
 A trailing ":g" runs that setting on a chunker created with RC_TILE_GROUPS=1 (group records
-and edge-range trimming for large windows too), ":G" with RC_TILE_GUIDED=1 (the guided tail).
+and edge-range trimming for large windows too).
 """
 import json
 import os
@@ -68,8 +68,6 @@ for s in settings:
     env = {'RC_TILE_STATIC': st, 'RC_TILE_CHUNK': ck}
     if ':g' in s[len(st) + len(ck) + 1:]:
         env['RC_TILE_GROUPS'] = '1'
-    if ':G' in s[len(st) + len(ck) + 1:]:
-        env['RC_TILE_GUIDED'] = '1'  # the shrinking tail units
     chunkers[s] = chunker_with(env)
 total, caps = chunkers[settings[0]].capacity(lens)
 cuts = torch.zeros(total, dtype=torch.int64, device='cuda')

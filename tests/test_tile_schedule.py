@@ -1,7 +1,7 @@
 """The tile kernel's work units (kernels.hip tile_units / TileUnits.range, through the host-only
-rc_tile_schedule): every schedule -- fully static, static share + dynamic units, and the guided
-tail of shrinking units (RC_TILE_GUIDED) -- must hand out each tile of the launch exactly once,
-in address order, in units of the promised sizes.  CPU only (no device)."""
+rc_tile_schedule): every schedule -- fully static, or a static share plus dynamic units -- must
+hand out each tile of the launch exactly once, in address order, in units of at most the
+promised size.  CPU only (no device)."""
 import ctypes
 
 import numpy as np
@@ -10,13 +10,13 @@ import pytest
 from replicat_amd import _lib
 
 
-def units(n_tiles, waves, permille=100, chunk=12, dyn_min=128, guided=0):
+def units(n_tiles, waves, permille=100, chunk=12, dyn_min=128):
     n = ctypes.c_uint64()
-    assert _lib.lib().rc_tile_schedule(n_tiles, waves, permille, chunk, dyn_min, guided, None,
-                                       0, ctypes.byref(n)) == 0
+    assert _lib.lib().rc_tile_schedule(n_tiles, waves, permille, chunk, dyn_min, None, 0,
+                                       ctypes.byref(n)) == 0
     r = np.zeros(2 * n.value, dtype=np.uint32)
-    assert _lib.lib().rc_tile_schedule(n_tiles, waves, permille, chunk, dyn_min, guided,
-                                       r.ctypes.data, n.value, ctypes.byref(n)) == 0
+    assert _lib.lib().rc_tile_schedule(n_tiles, waves, permille, chunk, dyn_min, r.ctypes.data,
+                                       n.value, ctypes.byref(n)) == 0
     return r.reshape(-1, 2).astype(np.int64)
 
 
@@ -28,11 +28,10 @@ CASES = [
 
 
 @pytest.mark.parametrize('n_tiles,waves', CASES)
-@pytest.mark.parametrize('permille,chunk,guided', [(100, 12, 0), (100, 12, 1), (250, 32, 1),
-                                                   (0, 7, 1), (0, 2, 1), (900, 3, 1),
-                                                   (1000, 12, 1), (100, 4, 1)])
-def test_units_partition_the_tiles(n_tiles, waves, permille, chunk, guided):
-    r = units(n_tiles, waves, permille, chunk, 128, guided)
+@pytest.mark.parametrize('permille,chunk', [(100, 12), (250, 32), (0, 7), (0, 2), (900, 3),
+                                            (1000, 12), (100, 4)])
+def test_units_partition_the_tiles(n_tiles, waves, permille, chunk):
+    r = units(n_tiles, waves, permille, chunk, 128)
     static, dyn = r[:waves], r[waves:]
     # static units: contiguous equal shares from tile 0; then the dynamic units in order
     assert ((0 <= r[:, 0]) & (r[:, 0] <= r[:, 1]) & (r[:, 1] <= n_tiles)).all()
@@ -45,12 +44,11 @@ def test_units_partition_the_tiles(n_tiles, waves, permille, chunk, guided):
     if len(dyn):
         sizes = dyn[:, 1] - dyn[:, 0]
         assert sizes.max() <= max(chunk, 2)
-        if guided and len(dyn) > 6 * waves:
-            # the last two units of each wave are 2 tiles: the launch's tail
-            assert (sizes[-waves:-1] <= 2).all()
-            assert sizes[:len(sizes) // 2].min() >= min(chunk, sizes.max())
+        # ~4 dynamic units per wave at least (a unit is the granularity of the launch's tail)
+        assert len(dyn) >= min(4 * waves, (n_tiles - static[:, 1].max()) // max(chunk, 2))
 
 
-def test_guided_adds_few_grabs():
-    plain, guided = units(3_874_000, 4096), units(3_874_000, 4096, guided=1)
-    assert len(plain) < len(guided) < len(plain) + 7 * 4096
+def test_static_below_the_dynamic_minimum():
+    """Fewer than 128 tiles per wave (the harness: 76): one static unit per wave."""
+    r = units(312_188, 4096)
+    assert len(r) == 4096 and (r[:, 1] - r[:, 0]).max() == 77
