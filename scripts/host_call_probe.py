@@ -40,13 +40,15 @@ for name, n, size, mn, mx in (('config3iii', 65536, 1 << 20, 2_000, 80_000),
                             pipelined=pip, end=pip and i == 2)
         ch.wait(hs)
         torch.cuda.synchronize()
-        host = []
+        host, marks = [], []
         t0 = time.perf_counter()
         for i in range(K):
             a = time.perf_counter()
             ch.chunk_device(ptrs, lens, last, cuts.data_ptr(), counts.data_ptr(), hs,
                             pipelined=pip, end=pip and i == K - 1)
-            host.append((time.perf_counter() - a) * 1e3)
+            b = time.perf_counter()
+            host.append((b - a) * 1e3)
+            marks.append((round((a - t0) * 1e3, 3), round((b - t0) * 1e3, 3)))
         ch.wait(hs)
         torch.cuda.synchronize()
         step = (time.perf_counter() - t0) * 1e3 / K
@@ -63,6 +65,8 @@ for name, n, size, mn, mx in (('config3iii', 65536, 1 << 20, 2_000, 80_000),
         out[f'{name}_{mode}'] = {'ms_per_step': round(step, 4),
                                  'host_ms_median': round(float(np.median(host)), 4),
                                  'host_ms_max': round(float(np.max(host)), 4),
-                                 'host_ms_gpu_idle': round(float(np.median(idle)), 4)}
+                                 'host_ms_gpu_idle': round(float(np.median(idle)), 4),
+                                 'pipelined_calls': ch.pipelined_calls(),
+                                 'call_marks_ms': marks}
         print(json.dumps({f'{name}_{mode}': out[f'{name}_{mode}']}), flush=True)
 print(json.dumps(out), flush=True)
