@@ -55,8 +55,10 @@ extern "C" {
                       pipelined callers use a non-blocking stream.  Calls the overlap does not
                       pay for run in sequence on hip_stream instead (a legal schedule of the
                       flag): chunkers with small windows (max_length below ~1 MB: the chain
-                      does not fit beside the tile kernel) and batches below ~128 tiles of
-                      16 KiB per tile-kernel wave (~8 GiB; the tile kernel's static schedule).
+                      does not fit beside the tile kernel) and batches with fewer 16 KiB
+                      tiles of needed bytes than the masked tile kernel has waves (~56 MiB on
+                      224 CUs; e.g. short streams whose keys are never needed: nothing to
+                      overlap the chain with).
                       RC_PIPE_ALL=1 in the environment pipelines every call.  The streams'
                       bytes and the outputs must stay allocated until the call is waited for:
                       a caching allocator (torch's) sees only the caller's stream, which a

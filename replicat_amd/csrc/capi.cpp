@@ -902,8 +902,8 @@ int rc_chunk_device(rc_chunker *ch, uint64_t n, const uint8_t *const *d_streams,
     // Round 4 re-measured launches on the static schedule (the harness: one 5.12 GB stream,
     // 76 tiles per wave), which round 3 also ran in sequence: on one allocation the tile kernel
     // takes 0.833 ms on 224 CUs as on 256, and pipelined steps 0.876 ms against 0.950 in sequence
-    // (profiles/r04/harness/harness_sched.log), so they pipeline now.  RC_PIPE_ALL=1 pipelines
-    // every call (tests, measurements).
+    // (profiles/r04/harness/harness_sched.log), so they pipeline now -- when the request has at
+    // least a tile per wave (below).  RC_PIPE_ALL=1 pipelines every call (tests, measurements).
     std::lock_guard<std::mutex> lock(ch->mu);
     DeviceGuard g(ch->device);
     const bool all = ch->knobs[knPipeAll] != 0;
@@ -915,6 +915,19 @@ int rc_chunk_device(rc_chunker *ch, uint64_t n, const uint8_t *const *d_streams,
         fprintf(stderr, "replicat_amd: pipelined calls run in sequence: %s\n", g_err);
     }
     if (ch->overlap_failed && !ch->tstream) pipelined = false;
+    // A request with fewer tiles than the masked tile launch has waves has next to nothing to
+    // overlap its chain with, and that chain would run on the reserved CUs only: config 3 (i)
+    // (65,536 x 1 MiB at the defaults: no key is ever needed) took 0.78 ms per step pipelined
+    // against 0.43 in sequence (profiles/r04/final/configs.log).  It runs in sequence.
+    if (pipelined && !all) {
+        uint64_t tiles = 0;
+        for (uint64_t i = 0; i < n; ++i) {
+            const uint64_t P = open ? lens[i] : (last_piece ? last_piece[i] : 0);
+            const uint64_t j = rc_keys_needed(ch->max_length, lens[i], P);
+            tiles += j ? j / kTileKeys + 1 : 0;
+        }
+        if (tiles < 16ull * ch->tile_cus) pipelined = false;
+    }
     ch->pipelined_calls += pipelined ? 1 : 0;
     Plan plan;
     Workspace &ws = acquire_ws(ch);

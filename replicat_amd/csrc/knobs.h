@@ -50,8 +50,8 @@ struct KnobSpec {
 // clang-format off
 inline constexpr KnobSpec kKnobTable[kKnobCount] = {
     {"RC_PIPE_ALL", 0, 0, 1, "0|1",
-     "1: every RC_PIPELINED request overlaps (otherwise small-window chunkers run in "
-     "sequence, capi.cpp rc_chunk_device)"},
+     "1: every RC_PIPELINED request overlaps (otherwise small-window chunkers and requests "
+     "under a tile per tile-kernel wave run in sequence, capi.cpp rc_chunk_device)"},
     {"RC_OVERLAP_CUS", 32, 1, 1024, nullptr,
      "CUs reserved for the chain kernels of pipelined calls (rc_chunker_overlap overrides; "
      "must be below the device's CU count)"},

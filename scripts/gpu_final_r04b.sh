@@ -21,7 +21,8 @@ timeout -k 10 400 python bench.py --gpus 2 --share-gpus --steps 10 --cpu-streams
 grep '^{' gpurun_out/final4/ranks2.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['n_gpus'], d['ranks_seen'], d['distinct_devices'], d['parity_sha256'], [r['parity'] for r in d['per_rank']], d['pipeline'].get('pipelined_steps'))"
 mkdir -p gpurun_out/prof
 BENCH="bench.py --steps 5 --warmup 1 --cpu-streams 0 --no-verify"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/trace -o run -- python3 $BENCH > gpurun_out/prof/trace.log 2>&1 || { echo trace failed; tail -20 gpurun_out/prof/trace.log; exit 6; }
+# the trace pass at the driver's 20 steps (the average then carries one warm-up launch in 22)
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof/trace -o run -- python3 bench.py --steps 20 --warmup 2 --cpu-streams 0 --no-verify > gpurun_out/prof/trace.log 2>&1 || { echo trace failed; tail -20 gpurun_out/prof/trace.log; exit 6; }
 grep '^{' gpurun_out/prof/trace.log | cut -c1-200
 timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "rc_tile|rc_read_probe" --output-format csv -d gpurun_out/prof/fetch -o run -- python3 $BENCH --calibrate > gpurun_out/prof/fetch.log 2>&1 || { echo "fetch pass failed rc=$?"; exit 7; }
 timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "rc_tile" --output-format csv -d gpurun_out/prof/write -o run -- python3 $BENCH > gpurun_out/prof/write.log 2>&1 || { echo "write pass failed rc=$?"; exit 7; }
