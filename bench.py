@@ -940,8 +940,9 @@ def main(argv=None, backend=Backend):
                          'unpipelined_ms_per_step': None if seq_ms is None else round(seq_ms, 3),
                          'note': 'steps are RC_PIPELINED calls: step k\'s edge + chain kernels '
                                  'run on the reserved CUs beside step k+1\'s tile kernel (the '
-                                 'library runs small-window batches in '
-                                 'sequence: pipelined_steps counts the overlapped ones); every '
+                                 'library runs small-window batches, and batches with fewer '
+                                 'tiles than the tile kernel has waves, in sequence: '
+                                 'pipelined_steps counts the overlapped ones); every '
                                  'step still computes every cut'} if pipelined else {'on': False},
             'higher_is_better': True,
             'scaling': 'weak',
