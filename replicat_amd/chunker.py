@@ -201,6 +201,7 @@ class QueueStream:
         check(lib().rc_stream_create(int(device), ctypes.byref(h)))
         self.handle, self.device = h.value, int(device)
         self._torch = None
+        self._pooled = False
 
     @classmethod
     def acquire(cls, device=None):
@@ -210,14 +211,17 @@ class QueueStream:
         with cls._lock:
             free = cls._pool.setdefault(int(device), [])
             if free:
-                return free.pop()
+                qs = free.pop()
+                qs._pooled = False
+                return qs
         return cls(device)
 
     def release(self):
         """Back to the pool (the caller's work on it may still be queued: the next user's work
-        follows it in stream order)."""
-        if self.handle:
-            with QueueStream._lock:
+        follows it in stream order).  Releasing twice pools it once."""
+        with QueueStream._lock:
+            if self.handle and not self._pooled:
+                self._pooled = True
                 QueueStream._pool.setdefault(self.device, []).append(self)
 
     @property
@@ -228,7 +232,11 @@ class QueueStream:
         return self._torch
 
     def close(self):
-        h, self.handle = self.handle, None
+        with QueueStream._lock:
+            if self._pooled:
+                QueueStream._pool[self.device].remove(self)
+                self._pooled = False
+            h, self.handle = self.handle, None
         self._torch = None
         if h:
             lib().rc_stream_destroy(h)
