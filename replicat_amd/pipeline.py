@@ -347,7 +347,7 @@ class DeviceSnapshotProducer:
                  params: Optional[bytes] = None, digest_size: int = 64,
                  batch_bytes: int = DEFAULT_BATCH, device=None, keep_contents: bool = True,
                  encryption: Optional[ChunkEncryption] = None, file_digests: str = 'auto',
-                 slots: int = 2, queues: str = 'own'):
+                 slots: int = 2, queues: str = 'own', read_threads: int = 4):
         import torch
         if device is None:
             device = _current_device()
@@ -359,6 +359,11 @@ class DeviceSnapshotProducer:
         if queues not in ('own', 'shared'):
             raise ValueError(f'queues must be own or shared, not {queues!r}')
         self.queues = queues
+        if int(read_threads) < 1:
+            raise ValueError('read_threads must be at least 1')
+        # a piece of a regular file is read as up to read_threads parallel positional reads
+        # (snapshot.PieceReader): the page-cache copy, not the device, bounds the producer
+        self.read_threads = int(read_threads)
         self.device = int(device)
         self.dev = torch.device('cuda', self.device)
         self.chunker = GpuChunker(min_length, max_length, normalize_params(params), device=self.device)
@@ -484,7 +489,8 @@ class DeviceSnapshotProducer:
         if not self._slots:
             raise RuntimeError('DeviceSnapshotProducer is closed')
         run = _Run(self, torch, files, zero_copy, sink)
-        reader = PieceReader(sort_files(paths), files, read, record=FileRecord, on_open=_fstat_size)
+        reader = PieceReader(sort_files(paths), files, read, record=FileRecord, on_open=_fstat_size,
+                             threads=self.read_threads)
         # fill / wait_cut / enqueue / collect_join: this thread; collect_wait / records /
         # host_digest_wait: the collector thread (overlapping the next fill)
         prof = self.profile = {'fill': 0.0, 'wait_cut': 0.0, 'enqueue': 0.0, 'collect_join': 0.0,

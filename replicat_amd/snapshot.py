@@ -12,6 +12,8 @@ files, parameters and key.
 import bisect
 import io
 import os
+import stat
+import threading
 from dataclasses import dataclass, field
 from typing import Iterator, List, Optional, Sequence, Tuple
 
@@ -40,6 +42,31 @@ def sort_files(paths: Sequence[os.PathLike]) -> List[str]:
     return sorted((str(p) for p in paths), key=lambda p: (os.stat(p).st_size, p))
 
 
+_READ_POOL = None
+_READ_POOL_LOCK = threading.Lock()
+READ_SPLIT = 4 << 20   # the smallest part of a piece read by one thread
+
+
+def _read_pool():
+    global _READ_POOL
+    with _READ_POOL_LOCK:
+        if _READ_POOL is None:
+            from concurrent.futures import ThreadPoolExecutor
+            _READ_POOL = ThreadPoolExecutor(max_workers=8, thread_name_prefix='rc-read')
+        return _READ_POOL
+
+
+def _pread_full(fd, view, off) -> int:
+    """Read view's length from fd at off (os.preadv releases the GIL); short only at EOF."""
+    done, n = 0, len(view)
+    while done < n:
+        r = os.preadv(fd, [view[done:]], off + done)
+        if r == 0:
+            break
+        done += r
+    return done
+
+
 class PieceReader:
     """The pieces replicat's _stream_files yields (repository.py:1413-1447) for already-sorted
     `paths`, read on demand into a caller's buffer: files in order, each in reads of at most
@@ -50,10 +77,18 @@ class PieceReader:
     `files` receives a record (``record(path=, stream_start=, stream_end=)``) when a file is
     opened, and its stream_end grows as the file is read; `on_open(record, file_object)` runs
     once per opened file.  Both stream_pieces and the device snapshot producer
-    (replicat_amd/pipeline.py) frame the stream through this one class."""
+    (replicat_amd/pipeline.py) frame the stream through this one class.
+
+    `threads` > 1: a piece of a regular file opened in binary mode is read as up to `threads`
+    parts of at least READ_SPLIT bytes, in parallel (positional reads from a shared pool) --
+    the same bytes as one read(PIECE) at the file's position: the piece ends at the first part
+    that comes back short (end of file), and the file's next piece starts after it."""
 
     def __init__(self, paths: Sequence[str], files: Optional[list] = None, read=None,
-                 record=None, on_open=None):
+                 record=None, on_open=None, threads: int = 1):
+        self._threads = max(1, int(threads))
+        self._fd = None     # a regular file read with positional reads (threads > 1)
+        self._off = 0
         self._paths = iter(paths)
         self.files = files if files is not None else []
         self._open = read if read else (lambda p: open(p, 'rb'))
@@ -95,10 +130,20 @@ class PieceReader:
             self.files.append(f)
             self._cm = self._open(path)
             self._src = self._cm.__enter__()
+            self._fd = None
+            if self._threads > 1 and isinstance(self._src, (io.BufferedReader, io.FileIO)):
+                try:
+                    fd = self._src.fileno()
+                    if stat.S_ISREG(os.fstat(fd).st_mode):
+                        self._fd, self._off = fd, self._src.tell()
+                except (OSError, ValueError):
+                    self._fd = None
             if self._on_open is not None:
                 self._on_open(f, self._src)
 
     def _read(self, mv) -> int:
+        if self._fd is not None:
+            return self._pread(mv)
         src = self._src
         if isinstance(src, (io.BufferedReader, io.BytesIO)):
             return src.readinto(mv[:PIECE]) or 0
@@ -106,16 +151,36 @@ class PieceReader:
         mv[:len(piece)] = piece
         return len(piece)
 
+    def _pread(self, mv) -> int:
+        want = min(PIECE, len(mv))
+        parts = max(1, min(self._threads, want // READ_SPLIT))
+        step = -(-want // parts)
+        ranges = [(a, min(a + step, want)) for a in range(0, want, step)]
+        if len(ranges) == 1:
+            got = [_pread_full(self._fd, mv[:want], self._off)]
+        else:
+            pool = _read_pool()
+            futs = [pool.submit(_pread_full, self._fd, mv[a:b], self._off + a) for a, b in ranges]
+            got = [f.result() for f in futs]
+        n = 0
+        for (a, b), g in zip(ranges, got):
+            n += g
+            if g < b - a:  # end of file: what later parts read (a file growing) is not this piece
+                break
+        self._off += n
+        return n
+
     def close(self):
+        self._fd = None
         cm, self._cm, self._src = self._cm, None, None
         if cm is not None:
             cm.__exit__(None, None, None)
 
 
 def stream_pieces(paths: Sequence[str], files_out: Optional[List[SnapshotFile]] = None,
-                  read=None) -> Iterator[bytes]:
+                  read=None, threads: int = 1) -> Iterator[bytes]:
     """The pieces replicat's _stream_files yields for already-sorted `paths`."""
-    reader = PieceReader(paths, files_out, read)
+    reader = PieceReader(paths, files_out, read, threads=threads)
     buf = bytearray(PIECE)
     try:
         while (got := reader.read_into(buf)) is not None:

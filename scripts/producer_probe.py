@@ -63,6 +63,9 @@ enc = ChunkEncryption(shared_key=os.urandom(32), shared_kdf_params=os.urandom(16
 variants = [('plain', {}), ('encrypted', {'encryption': enc})]
 if 'parallel_reads' in DeviceSnapshotProducer.__init__.__code__.co_varnames:
     variants.insert(1, ('plain_reads_in_line', {'parallel_reads': False}))
+HAS_RT = 'read_threads' in DeviceSnapshotProducer.__init__.__code__.co_varnames
+if HAS_RT:  # one positional read per piece (the default reads each piece as 4 parallel parts)
+    variants.insert(1, ('plain_1_reader', {'read_threads': 1}))
 for name, kw in variants:
     prod = DeviceSnapshotProducer(min_length=MIN, max_length=MAX, **kw)
     dt, res = timed(lambda: prod.run(paths))
@@ -109,11 +112,15 @@ def consume(prod, workers):
 
 
 if hasattr(DeviceSnapshotProducer, 'stream'):
-    for name, workers, kw in (('stream_release', 0, {}), ('stream_5_workers', 5, {}),
-                              ('stream_release_encrypted', 0, {'encryption': enc})):
+    svars = [('stream_release', 0, {}), ('stream_5_workers', 5, {}),
+             ('stream_release_encrypted', 0, {'encryption': enc})]
+    if HAS_RT:
+        svars.insert(1, ('stream_release_1_reader', 0, {'read_threads': 1}))
+        svars.insert(2, ('stream_release_3_slots', 0, {'slots': 3}))
+    for name, workers, kw in svars:
         prod = DeviceSnapshotProducer(min_length=MIN, max_length=MAX, **kw)
         dt, snap = timed(lambda: consume(prod, workers))
-        if not kw:
+        if not kw or kw.get('read_threads') or kw.get('slots'):
             assert [c.stream_end for c in snap.chunks] == [c.stream_end for c in plain.chunks]
             assert [c.digest for c in snap.chunks] == [c.digest for c in plain.chunks]
         print(json.dumps({'variant': name, 'bytes': total, 'files': nfiles,

@@ -11,10 +11,10 @@ import pytest
 from replicat_amd import pipeline, snapshot
 
 
-def _fill_all(paths, batch):
+def _fill_all(paths, batch, threads=1):
     files = []
     reader = snapshot.PieceReader(paths, files, None, record=pipeline.FileRecord,
-                                  on_open=pipeline._fstat_size)
+                                  on_open=pipeline._fstat_size, threads=threads)
     head = 64
     buf = np.zeros(head + batch + snapshot.PIECE + 64, dtype=np.uint8)
     look_buf = bytearray(snapshot.PIECE)
@@ -45,14 +45,16 @@ def _files(tmp_path, seed, n=24):
     return snapshot.sort_files(paths)
 
 
+@pytest.mark.parametrize('threads', [1, 4])
 @pytest.mark.parametrize('batch', [1 << 20, 5 << 20, 64 << 20])
-def test_fill_batch_is_the_reference_stream(tmp_path, batch):
+def test_fill_batch_is_the_reference_stream(tmp_path, batch, threads):
     """Batches of whole pieces: concatenated, the reference's stream; every batch but the last
     holds at least `batch` bytes and ends at a piece boundary; the closed-file count of a batch
     is the number of files whose bytes all lie in it or before; the last piece's offset is where
-    the stream's final piece starts (P of the final batch)."""
+    the stream's final piece starts (P of the final batch).  threads=4: pieces of regular files
+    read as parallel positional parts (the producer's default)."""
     paths = _files(tmp_path, batch)
-    batches, pieces, files = _fill_all(paths, batch)
+    batches, pieces, files = _fill_all(paths, batch, threads)
     pieces_ref = list(snapshot.stream_pieces(paths))
     assert b''.join(b for b, _, _ in batches) == b''.join(pieces_ref)
     assert [ln for _, _, ln in pieces] == [len(p) for p in pieces_ref]
@@ -144,3 +146,29 @@ def test_record_release_is_idempotent():
     import threading
     recs[-1].release()
     assert lease.wait(threading.Event()) is True
+
+
+@pytest.mark.parametrize('threads', [2, 3, 4, 8])
+def test_parallel_piece_reads_are_read_piece(tmp_path, threads):
+    """PieceReader(threads > 1) against one read(PIECE) per piece (stream_pieces, threads=1) at
+    the sizes where parts meet pieces: a piece of exactly PIECE, one byte either side, a part
+    boundary (READ_SPLIT multiples), empty and tiny files, files opened by a `read` hook that
+    are not regular buffered files (BytesIO: read as before)."""
+    import io
+    P, S = snapshot.PIECE, snapshot.READ_SPLIT
+    sizes = [0, 1, S - 1, S, S + 1, 3 * S + 5, P - 1, P, P + 1, 2 * P + S - 3]
+    paths = []
+    for i, n in enumerate(sizes):
+        p = tmp_path / ('g%02d' % i)
+        p.write_bytes(os.urandom(n))
+        paths.append(p)
+    paths = snapshot.sort_files(paths)
+    ref_files, got_files = [], []
+    ref = list(snapshot.stream_pieces(paths, ref_files))
+    got = list(snapshot.stream_pieces(paths, got_files, threads=threads))
+    assert [len(x) for x in got] == [len(x) for x in ref]
+    assert got == ref
+    assert got_files == ref_files
+    hooked = list(snapshot.stream_pieces(
+        paths, read=lambda p: io.BytesIO(open(p, 'rb').read()), threads=threads))
+    assert hooked == ref
