@@ -117,10 +117,11 @@ if hasattr(DeviceSnapshotProducer, 'stream'):
     if HAS_RT:
         svars.insert(1, ('stream_release_1_reader', 0, {'read_threads': 1}))
         svars.insert(2, ('stream_release_3_slots', 0, {'slots': 3}))
+        svars.insert(3, ('stream_release_2gib_batches', 0, {'batch_bytes': 2 << 30}))
     for name, workers, kw in svars:
         prod = DeviceSnapshotProducer(min_length=MIN, max_length=MAX, **kw)
         dt, snap = timed(lambda: consume(prod, workers))
-        if not kw or kw.get('read_threads') or kw.get('slots'):
+        if not kw or kw.get('read_threads') or kw.get('slots') or kw.get('batch_bytes'):
             assert [c.stream_end for c in snap.chunks] == [c.stream_end for c in plain.chunks]
             assert [c.digest for c in snap.chunks] == [c.digest for c in plain.chunks]
         print(json.dumps({'variant': name, 'bytes': total, 'files': nfiles,
