@@ -253,6 +253,7 @@ struct rc_chunker {
     uint32_t reserve_req = 0;  // rc_chunker_overlap (0: RC_OVERLAP_CUS, default 32)
     uint32_t reserve = 0, tile_cus = 0;  // of the streams below (0: not created)
     hipStream_t tstream = nullptr, xstream = nullptr;
+    hipStream_t tstream2 = nullptr;  // RC_TILE_STREAMS=2: the odd workspace's tile kernels
     hipStream_t fstream = nullptr;  // RC_PIPELINE_END calls' edge and chain kernels: every CU
     hipEvent_t in_ev[2] = {nullptr, nullptr}, tiled[2] = {nullptr, nullptr};
     uint64_t pipelined_calls = 0;  // RC_PIPELINED requests that ran on the two streams
@@ -509,7 +510,7 @@ int upload_and_launch(rc_chunker *ch, Workspace &ws, const Plan &plan, ChainPara
     // caller's stream waits for nothing (rc_chunk_wait)
     hipStream_t ts = stream, xs = stream;
     if (pipelined) {
-        ts = ch->tstream;
+        ts = wi == 1 && ch->tstream2 ? ch->tstream2 : ch->tstream;
         // RC_PIPELINE_END: nothing follows for this chain to overlap, so it runs on every CU
         xs = end ? ch->fstream : ch->xstream;
         // the inputs: nothing to wait for when the caller's stream has no work pending (each
@@ -603,6 +604,11 @@ int setup_overlap(rc_chunker *ch) {
     if (want == 0 || (int)want >= cus)
         return fail(RC_ERR_ARGUMENT, "overlap: %u reserved CUs of %d", want, cus);
     if (ch->tstream) {  // a different split: retire the old pair
+        if (ch->tstream2) {
+            HIP_TRY(hipStreamSynchronize(ch->tstream2));
+            (void)hipStreamDestroy(ch->tstream2);
+            ch->tstream2 = nullptr;
+        }
         HIP_TRY(hipStreamSynchronize(ch->tstream));
         HIP_TRY(hipStreamSynchronize(ch->xstream));
         (void)hipStreamDestroy(ch->tstream);
@@ -618,6 +624,13 @@ int setup_overlap(rc_chunker *ch) {
         ch->tstream = ch->xstream = nullptr;
         return fail(RC_ERR_HIP, "hipExtStreamCreateWithCUMask failed: %s", hipGetErrorString(ex));
     }
+    // RC_TILE_STREAMS=2: odd calls' tile kernels on a second stream with the same mask (a queue
+    // of its own), so that a call's tile kernel is not held behind the previous one's last
+    // workgroups: its workgroups take the CUs the previous launch leaves (their workspaces are
+    // distinct; a call's chain still follows its own tile kernel and the previous chain)
+    if (ch->knobs[knTileStreams] == 2 &&
+        hipExtStreamCreateWithCUMask(&ch->tstream2, (uint32_t)tm.size(), tm.data()) != hipSuccess)
+        ch->tstream2 = nullptr;  // one tile stream: still correct
     if (!ch->fstream) HIP_TRY(hipStreamCreateWithFlags(&ch->fstream, hipStreamNonBlocking));
     for (int i = 0; i < 2; ++i) {
         if (!ch->in_ev[i]) HIP_TRY(hipEventCreateWithFlags(&ch->in_ev[i], hipEventDisableTiming));
@@ -784,6 +797,7 @@ void rc_chunker_destroy(rc_chunker *ch) {
         ch->h_out.release();
         if (ch->cstream) (void)hipStreamDestroy(ch->cstream);
         if (ch->tstream) (void)hipStreamDestroy(ch->tstream);
+        if (ch->tstream2) (void)hipStreamDestroy(ch->tstream2);
         if (ch->xstream) (void)hipStreamDestroy(ch->xstream);
         if (ch->fstream) (void)hipStreamDestroy(ch->fstream);
         for (auto e : ch->uploaded)

@@ -35,6 +35,7 @@ enum Knob : int {
     knB2LaneOnly,     // RC_B2_LANE_ONLY
     knProbeBlock,     // RC_PROBE_BLOCK
     knGcmDebug,       // RC_GCM_DEBUG
+    knTileStreams,    // RC_TILE_STREAMS
     kKnobCount
 };
 
@@ -87,6 +88,9 @@ inline constexpr KnobSpec kKnobTable[kKnobCount] = {
      "read probe: interleaved static runs of this many tiles (0: the tile kernel's schedule)"},
     {"RC_GCM_DEBUG", 0, 0, 1, "0|1",
      "1: stamp every host step of an AES-GCM call on stderr"},
+    {"RC_TILE_STREAMS", 1, 1, 2, nullptr,
+     "CU-masked tile streams of pipelined calls: 2 alternates them, so a call's tile kernel "
+     "may start on CUs the previous one has left"},
 };
 // clang-format on
 

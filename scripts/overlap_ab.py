@@ -5,8 +5,10 @@ median wall time per step over K back-to-back steps, the tile kernel's HIP-event
 edge + chain time are printed.  Every setting must give the same cut lists.
 
     python scripts/overlap_ab.py [config] [rounds] [setting ...]   setting = seq | pR (R CUs)
-                                          [@STATIC:CHUNK] (tile schedule: a chunker created
-                                          with RC_TILE_STATIC / RC_TILE_CHUNK, knobs.h)
+                                          | pRx2 (R CUs, RC_TILE_STREAMS=2: two tile streams)
+                                          [@STATIC:CHUNK[:DYN_MIN]] (tile schedule: a chunker
+                                          created with RC_TILE_STATIC / RC_TILE_CHUNK /
+                                          RC_TILE_DYN_MIN, knobs.h)
     python scripts/overlap_ab.py 2 4 seq p8 p16 p32
 """
 import json
@@ -63,12 +65,25 @@ def chunker_with(env):
                 os.environ[k] = v
 
 
+def chunker_key(s):
+    base, _, sched = s.partition('@')
+    return sched + ('x2' if base.endswith('x2') else '')
+
+
 chunkers = {}
 for s in settings:
-    sched = s.partition('@')[2]
-    if sched not in chunkers:
-        st, ck = sched.split(':') if sched else (None, None)
-        chunkers[sched] = chunker_with({'RC_TILE_STATIC': st, 'RC_TILE_CHUNK': ck} if sched else {})
+    key = chunker_key(s)
+    if key not in chunkers:
+        sched = s.partition('@')[2]
+        env = {}
+        if sched:  # STATIC:CHUNK[:DYN_MIN]
+            parts = sched.split(':')
+            env.update({'RC_TILE_STATIC': parts[0], 'RC_TILE_CHUNK': parts[1]})
+            if len(parts) > 2:
+                env['RC_TILE_DYN_MIN'] = parts[2]
+        if key.endswith('x2'):
+            env['RC_TILE_STREAMS'] = '2'
+        chunkers[key] = chunker_with(env)
 ch = next(iter(chunkers.values()))
 total, caps = ch.capacity(lens)
 cuts = torch.zeros(total, dtype=torch.int64, device='cuda')
@@ -83,10 +98,10 @@ for r in range(rounds):
     order = settings if r % 2 == 0 else settings[::-1]
     for s in order:
         base, _, sched = s.partition('@')  # ...@STATIC:CHUNK -- the tile schedule's chunker
-        ch = chunkers[sched]
+        ch = chunkers[chunker_key(s)]
         pipe = base != 'seq'
         if pipe:
-            ch.overlap(int(base[1:].split(':')[0]))
+            ch.overlap(int(base[1:].split(':')[0].removesuffix('x2')))
 
         def step():
             ch.chunk_device(ptrs, lens, last, cuts.data_ptr(), counts.data_ptr(), hs,
