@@ -108,10 +108,13 @@ def test_golden_streams_pipelined(pipe_all):
             assert g == e['ends'], (e['data'], e['size'])
 
 
-def test_back_to_back_batches(pipe_all):
+@pytest.mark.parametrize('tile_streams', [1, 2])
+def test_back_to_back_batches(pipe_all, tile_streams, monkeypatch):
     """Eight pipelined calls over different batches (workspaces alternate while chains run
     beside later tile kernels), each with its own outputs, then mixed with sequential calls;
-    one wait, then every batch against its sequential result."""
+    one wait, then every batch against its sequential result.  tile_streams=2
+    (RC_TILE_STREAMS): consecutive tile kernels on two masked streams, free to overlap."""
+    monkeypatch.setenv('RC_TILE_STREAMS', str(tile_streams))
     ch = GpuChunker(MIN_LENGTH, MAX_LENGTH, b'\xff' * 16)
     ch.overlap(16)
     n, size = 32, 16 * MIB
