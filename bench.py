@@ -365,7 +365,7 @@ def _pool_map(fn, jobs):
         return pool.map(fn, jobs)
 
 
-def cpu_baseline(n_streams, size, seed, procs, min_len=MIN_LEN, max_len=MAX_LEN):
+def cpu_baseline(n_streams, size, seed, procs, min_len=MIN_LEN, max_len=MAX_LEN, extras=True):
     """the reference's native scan on the box's host cores, one process per
     core, over `n_streams` of the same synthetic streams; the adapter-loop rate beside it; and
     the speed ratio of the reference build to the oracle port on the same sample."""
@@ -387,7 +387,7 @@ def cpu_baseline(n_streams, size, seed, procs, min_len=MIN_LEN, max_len=MAX_LEN)
                      f'0..{n_streams - 1}), one process per core, native next_cut scan time of '
                      f'the slowest process ({busiest:.2f} s; {wall:.1f} s wall incl. data '
                      f'generation)'}
-    if kind == 'reference':
+    if kind == 'reference' and extras:
         # the adapter loop: one stream per core (16 MiB pieces), and the reference-vs-port
         # time ratio on two streams in this process
         k = min(procs, n_streams)
@@ -418,15 +418,30 @@ def harness_cpu(pieces, min_len, max_len):
 
 # ---------------------------------------------------------------- PMC traffic (profiles/)
 
-def pmc_traffic(config, n, size, build_id):
+def workload_key(args, n, size, custom, long):
+    """The profiles/ name of a line's workload (one rocprofv3 PMC entry per BASELINE line), or
+    None for a workload without one (custom sizes or parameters; 3 (i) reads nothing)."""
+    if custom or args.streams is not None or args.stream_mib is not None:
+        return None
+    if args.config == '2':
+        return 'config2' if args.key == 'ff' else 'config2_seeded'
+    if args.key != 'ff':
+        return None
+    return {'3ii': 'config3ii' if long is not None and long.world == 1 else None,
+            '3iii': 'config3iii', '4': 'config4', '5': 'config5',
+            'harness': 'harness'}.get(args.config)
+
+
+def pmc_traffic(workload, build_id):
     """HBM bytes per rc_tile_kernel launch from the committed rocprofv3 PMC summary of this same
-    command (scripts/gpu_profile.sh -> scripts/summarize_profile.py: separate --pmc passes,
+    workload (scripts/gpu_pmc_all.sh -> scripts/summarize_profile.py: separate --pmc passes,
     FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM, WRITE_SIZE as is).  Only a summary of the
     SAME library build counts: it is stamped with rc_build_id(), and a stale one is refused.
     bench.py cannot read counters itself (that needs rocprofv3)."""
-    if not (config == '2' and n == 1024 and size == 64 << 20):
+    if workload is None:
         return None, 'no PMC summary for this workload'
     import glob
+    stale = None
     for f in sorted(glob.glob(os.path.join(ROOT, 'profiles', 'r*', 'pmc_summary.json')),
                     reverse=True):
         try:
@@ -434,14 +449,20 @@ def pmc_traffic(config, n, size, build_id):
                 d = json.load(fh)
         except (OSError, ValueError):
             continue
-        t = d.get('rc_tile_kernel', {})
-        if d.get('workload') != 'config2' or 'hbm_read_bytes_corrected' not in t:
+        if workload in d.get('workloads', {}):
+            t = d['workloads'][workload].get('rc_tile_kernel', {})
+        elif d.get('workload') == workload:  # the round-4 layout (config 2 only)
+            t = d.get('rc_tile_kernel', {})
+        else:
+            continue
+        if 'hbm_read_bytes_corrected' not in t:
             continue
         if d.get('build_id') != build_id:
-            return None, f'{os.path.relpath(f, ROOT)} is of build {d.get("build_id")}, not {build_id}'
+            stale = stale or f'{os.path.relpath(f, ROOT)} is of build {d.get("build_id")}, not {build_id}'
+            continue
         return (t['hbm_read_bytes_corrected'] + t.get('hbm_write_bytes', 0.0),
-                os.path.relpath(f, ROOT))
-    return None, 'no PMC summary under profiles/'
+                os.path.relpath(f, ROOT) + f' [{workload}]')
+    return None, stale or f'no PMC summary of {workload} under profiles/'
 
 
 # ------------------------------------------------------------------- config 5 (dedup)
@@ -635,6 +656,9 @@ def check_parity(args, n, size, rank, long, edit, ends, digest):
     own shard (tests/golden/ranks.json: every rank of an up-to-8-GPU line; rank 0's entries are
     the single-GPU fixtures), or (None, None) when no fixture covers the workload.  main() ANDs
     the ranks' flags into the line's (null when any rank has none)."""
+    cfg = CONFIGS[args.config]
+    if (args.min_length not in (None, cfg[2])) or (args.max_length not in (None, cfg[3])):
+        return None, None  # every fixture is of the config's own chunk parameters
     G = _golden()
     R = G.load('ranks.json')
     ff = args.key == 'ff'
@@ -891,8 +915,7 @@ def main(argv=None, backend=Backend):
     if rank == 0:
         from replicat_amd.chunker import build_id
         bid = build_id()
-        traffic, traffic_src = pmc_traffic(args.config, n, size, bid) if args.key == 'ff' \
-            else (None, 'seeded key: no PMC summary')
+        traffic, traffic_src = pmc_traffic(workload_key(args, n, size, custom, long), bid)
         roof = roofline(bytes_per_step, bytes_needed(max_len, lens, last), tile_ms / calls,
                         edge_ms / calls, chain_ms / calls, traffic, traffic_src, bid)
         if piped:
@@ -923,6 +946,15 @@ def main(argv=None, backend=Backend):
             if ends is not None:
                 cpu['matches_gpu'] = bool(all(np.array_equal(np.asarray(cpu_ends[i], np.uint64),
                                                              ends[i]) for i in cpu_ends))
+            if seen > procs and not args.cpu_procs:
+                # beside the per-GPU share: the same scan on EVERY core of the affinity mask
+                # (the box's whole host; value stays the share)
+                whole, whole_ends = cpu_baseline(sample, size, synth.DEFAULT_SEED, seen,
+                                                 extras=False)
+                cpu['whole_mask'] = {k: whole[k] for k in ('value', 'unit', 'cores', 'kind',
+                                                           'sample')}
+                cpu['whole_mask']['matches_share'] = all(
+                    list(whole_ends[i]) == list(cpu_ends[i]) for i in cpu_ends)
         elif harness is not None and args.cpu_streams != 0:
             cpu, lengths = harness_cpu(harness, min_len, max_len)
             if cpu is not None and ends is not None:

@@ -140,7 +140,11 @@ int rc_chunk_wait(rc_chunker *ch, void *hip_stream);
  * it is a BLOCKING stream: work on the legacy NULL stream synchronises with it.  The snapshot
  * producer's batch streams use it so that consecutive batches' digests (each ending with a
  * ~55 ms BLAKE2b chain) overlap at HIP's default queue count.  rc_stream_destroy waits for the
- * stream's work; streams still alive at process exit are destroyed then. */
+ * stream's work; streams still alive at process exit are destroyed then (the library's exit
+ * hook).  Do NOT destroy a stream another runtime has wrapped and may still record events on
+ * (torch's caching allocator records one on every stream a freed tensor was used on, possibly
+ * long after): leave it to the exit hook -- replicat_amd.chunker.QueueStream.close() retires
+ * such a stream instead of destroying it.  Each stream holds one hardware queue of its own. */
 int rc_stream_create(int device, void **out_stream);
 void rc_stream_destroy(void *stream);
 
@@ -150,6 +154,13 @@ void rc_stream_destroy(void *stream);
 int rc_chunk_host(rc_chunker *ch, uint64_t n, const uint8_t *const *streams,
                   const uint64_t *lens, const uint64_t *last_piece, uint32_t flags,
                   uint64_t *cuts, int64_t *counts);
+
+/* Waits for the chunker's calls so far and reports a tile-kernel fail-safe stop: with
+ * workgroup grabs (RC_TILE_GROUP) a wave that waited ~1 s for its group's grab to be published
+ * stops rather than hang the GPU, leaving that launch's records incomplete.  RC_OK, or
+ * RC_ERR_HIP with rc_last_error() naming it.  (Never observed; the tests call it after every
+ * dynamic-schedule run.)  Not a reference interface: replicat has no device. */
+int rc_chunker_check(rc_chunker *ch);
 
 /* Kernel timing, for bench.py's roofline: while enabled, every rc_chunk_device call records
  * HIP events on the launch stream before the tile kernel, between it and the edge kernel, and

@@ -49,6 +49,7 @@ SIGNATURES = {
     'rc_chunker_overlap': (_int, [_p, _u32]),
     'rc_chunker_overlap_cus': (_u32, [_p]),
     'rc_chunker_pipelined_calls': (_u64, [_p]),
+    'rc_chunker_check': (_int, [_p]),
     'rc_chunk_wait': (_int, [_p, _p]),
     'rc_stream_create': (_int, [_int, ctypes.POINTER(_p)]),
     'rc_stream_destroy': (None, [_p]),

@@ -112,6 +112,11 @@ class GpuChunker:
         """Pipelined requests so far that ran on the two streams (the others in sequence)."""
         return int(lib().rc_chunker_pipelined_calls(self._h))
 
+    def check(self):
+        """Wait for every call so far and raise if a tile kernel took its fail-safe stop (a
+        workgroup grab never published: rc_chunker_check)."""
+        check(lib().rc_chunker_check(self._h))
+
     def wait(self, stream=0):
         """Make a HIP stream wait for every call so far (pipelined or not)."""
         check(lib().rc_chunk_wait(self._h, stream or None))
@@ -186,12 +191,16 @@ class QueueStream:
 
     Lifetime: torch's caching allocator records events on the streams a tensor was used on
     (``record_stream``) when it frees the tensor, possibly much later, so a stream torch has
-    seen must outlive every such tensor.  Take streams from the process-wide pool
-    (``QueueStream.acquire`` / ``release``): pooled streams are reused, never destroyed while
-    the process runs, and released by the library's exit hook after Python's own finalisation.
-    ``close()`` destroys a stream at once -- only for one torch never used."""
+    seen must outlive every such tensor (round 4: a destroyed stream crashed a later test).
+    Take streams from the process-wide pool (``QueueStream.acquire`` / ``release``): pooled
+    streams are reused, never destroyed while the process runs, and released by the library's
+    exit hook after Python's own finalisation.  ``close()`` destroys a stream at once only if
+    torch never wrapped it (``torch`` never taken); a wrapped stream is retired instead -- out of
+    the pool, never handed out again, destroyed by the exit hook like the pooled ones
+    (INTEGRATION §7)."""
 
     _pool = {}
+    _retired = []  # closed streams torch has seen: kept until the library's exit hook
     _lock = threading.Lock()
 
     def __init__(self, device=None):
@@ -201,6 +210,7 @@ class QueueStream:
         check(lib().rc_stream_create(int(device), ctypes.byref(h)))
         self.handle, self.device = h.value, int(device)
         self._torch = None
+        self._wrapped = False  # torch has seen this stream (it may record events on it)
         self._pooled = False
 
     @classmethod
@@ -226,17 +236,25 @@ class QueueStream:
 
     @property
     def torch(self):
+        if self.handle is None:
+            raise RuntimeError('QueueStream is closed')
         if self._torch is None:
             import torch
             self._torch = torch.cuda.ExternalStream(self.handle, device=self.device)
+            self._wrapped = True
         return self._torch
 
     def close(self):
+        """Done with the stream for good.  Destroyed now if torch never wrapped it; otherwise
+        retired (torch may still record an event on it when it frees a tensor used there)."""
         with QueueStream._lock:
             if self._pooled:
                 QueueStream._pool[self.device].remove(self)
                 self._pooled = False
             h, self.handle = self.handle, None
+            if h and self._wrapped:
+                QueueStream._retired.append((h, self._torch))  # the exit hook destroys h
+                h = None
         self._torch = None
         if h:
             lib().rc_stream_destroy(h)

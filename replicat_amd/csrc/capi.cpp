@@ -472,6 +472,19 @@ int ensure_ctr(Workspace &ws, hipStream_t st) {
     return 0;
 }
 
+// The tile kernel's fail-safe flag (kernels.hip UnitGrab::next, word 32 of the counter buffer):
+// a wave that waited ~1 s for a grab published through LDS stopped instead of hanging.  Blocking
+// read; the caller has synchronised.
+int grab_fault(Workspace &ws) {
+    if (!ws.d_ctr.p) return 0;
+    uint32_t flag = 0;
+    HIP_TRY(hipMemcpy(&flag, static_cast<uint32_t *>(ws.d_ctr.p) + 32, 4, hipMemcpyDeviceToHost));
+    if (flag)
+        return fail(RC_ERR_HIP, "tile kernel: a workgroup grab was never published (fail-safe "
+                                "stop; records of that launch are incomplete)");
+    return 0;
+}
+
 // A launch sequence that failed after its tile kernel was queued: wait for whatever it queued
 // (this workspace's buffers are reused by the call after next) and leave the grab counter to be
 // re-zeroed -- its edge kernel, which zeroes it, may never have been queued.  Returns `rc`.
@@ -737,6 +750,7 @@ int rc_chunker_create(uint64_t min_length, uint64_t max_length, const uint8_t *k
     ch->sched.permille = (uint32_t)knobs[knTileStatic];
     ch->sched.chunk = (uint32_t)knobs[knTileChunk];
     ch->sched.dyn_min = (uint32_t)knobs[knTileDynMin];
+    ch->sched.group = (uint32_t)knobs[knTileGroup];
     ch->k0 = k0;
     ch->k1 = k1;
     ch->device = device;
@@ -773,6 +787,9 @@ void rc_chunker_destroy(rc_chunker *ch) {
     if (!ch) return;
     rc_untrack(ch);
     {
+        // a call still running on another thread (a daemon thread when the exit hook runs)
+        // finishes first: its buffers and streams go only after it
+        std::lock_guard<std::mutex> lock(ch->mu);
         DeviceGuard g(ch->device);
         (void)hipDeviceSynchronize();
         if (ch->d_tables) (void)hipFree(ch->d_tables);
@@ -992,6 +1009,17 @@ uint32_t rc_chunker_overlap_cus(const rc_chunker *ch) { return ch ? ch->reserve 
 
 uint64_t rc_chunker_pipelined_calls(const rc_chunker *ch) { return ch ? ch->pipelined_calls : 0; }
 
+int rc_chunker_check(rc_chunker *ch) {
+    if (!ch) return fail(RC_ERR_ARGUMENT, "null chunker");
+    std::lock_guard<std::mutex> lock(ch->mu);
+    DeviceGuard g(ch->device);
+    for (auto &w : ch->ws) {
+        if (w.pending) HIP_TRY(hipEventSynchronize(w.done));
+        if (int rc = grab_fault(w)) return rc;
+    }
+    return RC_OK;
+}
+
 int rc_chunk_wait(rc_chunker *ch, void *hip_stream) {
     if (!ch) return fail(RC_ERR_ARGUMENT, "null chunker");
     std::lock_guard<std::mutex> lock(ch->mu);
@@ -1141,6 +1169,9 @@ int rc_tile_records(rc_chunker *ch, uint64_t n, const uint8_t *const *d_streams,
     HIP_TRY(hipMemcpy(ws.d_desc.p, ws.h_desc.p, plan.bytes, hipMemcpyHostToDevice));
     if (int rc = ensure_ctr(ws, nullptr)) return rc;
     GroupRecord *d_grp = ch->groups ? group_records(ws, plan) : nullptr;
+    // poison the records first: a tile the schedule never ran shows as 0xabab.. keys
+    if (plan.n_tiles)
+        HIP_TRY(hipMemset(ws.d_records.p, 0xab, (plan.n_tiles + 1) * sizeof(TileRecord)));
     if (rc_launch_tiles(ch->d_tables, desc_view(ws.d_desc.p, n), n, plan.n_tiles,
                         static_cast<TileRecord *>(ws.d_records.p), d_grp,
                         group_hot_threshold(ch->window), tie_lists(ws, plan),
@@ -1148,6 +1179,7 @@ int rc_tile_records(rc_chunker *ch, uint64_t n, const uint8_t *const *d_streams,
                         ch->sched))
         return abandon_launch(ws, nullptr, nullptr, fail(RC_ERR_HIP, "%s", rc_launch_error()));
     HIP_TRY(hipDeviceSynchronize());
+    if (int rc = grab_fault(ws)) return rc;
     std::vector<TileRecord> h(plan.n_tiles);
     std::vector<GroupRecord> hg(plan.n_tiles, GroupRecord{~0ull, {~0ull, ~0ull, ~0ull, ~0ull}, 0ull});
     if (plan.n_tiles) {
@@ -1207,7 +1239,14 @@ int rc_timing_read(rc_chunker *ch, double *phase_a_ms, double *phase_b_ms, uint6
 int rc_read_probe(const uint8_t *d_src, uint64_t nbytes, uint32_t *d_out, void *hip_stream) {
     if (nbytes && (!d_src || !d_out)) return fail(RC_ERR_ARGUMENT, "null argument");
     if (reinterpret_cast<uintptr_t>(d_src) & 15) return fail(RC_ERR_ALIGN, "source not 16-byte aligned");
-    if (rc_launch_read_probe(d_src, nbytes, d_out, (uint32_t)process_knobs()[knProbeBlock], hip_stream))
+    // the tile kernel's schedule as a chunker created now would run it (the process's knobs)
+    const Knobs &k = process_knobs();
+    TileSched sched;
+    sched.permille = (uint32_t)k[knTileStatic];
+    sched.chunk = (uint32_t)k[knTileChunk];
+    sched.dyn_min = (uint32_t)k[knTileDynMin];
+    sched.group = (uint32_t)k[knTileGroup];
+    if (rc_launch_read_probe(d_src, nbytes, d_out, (uint32_t)k[knProbeBlock], sched, hip_stream))
         return fail(RC_ERR_HIP, "%s", rc_launch_error());
     return RC_OK;
 }

@@ -325,6 +325,9 @@ void rc_gcm_destroy(rc_gcm *g) {
     if (!g) return;
     rc_untrack(g);
     {
+        // a call still running on another thread (a daemon thread when the exit hook runs)
+        // finishes first: its buffers and streams go only after it
+        std::lock_guard<std::mutex> lock(g->mu);
         DeviceGuard guard(g->device);
         (void)hipDeviceSynchronize();
         for (auto &w : g->ws) {

@@ -273,6 +273,9 @@ void rc_blake2b_destroy(rc_hasher *h) {
     if (!h) return;
     rc_untrack(h);
     {
+        // a call still running on another thread (a daemon thread when the exit hook runs)
+        // finishes first: its buffers and streams go only after it
+        std::lock_guard<std::mutex> lock(h->mu);
         Guard g(h->device);
         (void)hipDeviceSynchronize();
         for (auto &w : h->ws) {

@@ -117,6 +117,7 @@ struct TileSched {
     uint32_t permille = 100;
     uint32_t chunk = 12;
     uint32_t dyn_min = 128;
+    uint32_t group = 0;  // units per workgroup grab (kernels.hip UnitGrab); 0: per-wave grabs
 };
 
 // splitmix64 finaliser (replicat_amd/synth.py)
@@ -159,8 +160,8 @@ int rc_launch_fill(uint8_t *d_dst, uint64_t nbytes, uint64_t seed, uint64_t stre
                    uint64_t word0, void *stream);
 int rc_launch_fill_streams(uint8_t *d_dst, uint64_t n, uint64_t nbytes, uint64_t slot,
                            uint64_t seed, uint64_t id0, uint64_t id_step, void *stream);
-// block: 0 = the tile kernel's default schedule, else interleaved static runs of `block` tiles
+// block: 0 = the tile kernel's schedule `sched`, else interleaved static runs of `block` tiles
 int rc_launch_read_probe(const uint8_t *d_src, uint64_t nbytes, uint32_t *d_out, uint32_t block,
-                         void *stream);
+                         rc::TileSched sched, void *stream);
 const char *rc_launch_error(void);
 }

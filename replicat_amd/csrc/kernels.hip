@@ -457,7 +457,7 @@ struct TileCursor {
     }
 };
 
-__device__ __forceinline__ void stage_tile_tables(const KeyTables *tab) {
+__device__ __forceinline__ void stage_tile_tables_nb(const KeyTables *tab) {
     // the 32x replicated prefilter tables and the exact tables.  Each thread loads its table
     // entries once (all loads in flight together), then writes the 32 copies, starting at a
     // lane-dependent copy so that a wave's stores spread over the banks.
@@ -481,7 +481,6 @@ __device__ __forceinline__ void stage_tile_tables(const KeyTables *tab) {
     uint64_t *full = reinterpret_cast<uint64_t *>(s_tile_lds + kFullOff / 4);
     const uint64_t *gfull = &tab->tl[0][0];
     for (uint32_t i = threadIdx.x; i < 2048u; i += nt) full[i] = gfull[i];
-    __syncthreads();
 }
 
 // Group bounds of one tile from the lanes' packed per-group top-16 maxima (gpk: group 2i in the
@@ -513,6 +512,8 @@ __device__ __forceinline__ GroupRecord tile_groups(const uint32_t (&gpk)[(G + 1)
 // (tile_units).
 struct TileUnits {  // tile indices fit 32 bits (the tie lists store them as u32)
     uint32_t n_tiles, nw, s0, chunk, dyn0, n_units;
+    uint32_t gshift;    // group grabs (UnitGrab): 2^gshift dynamic units per global grab
+    uint32_t n_groups;  // group grabs: global grab values below this hold units; 0: per-wave grabs
     __device__ __host__ void range(uint32_t u, uint32_t &b, uint32_t &e) const {
         if (u < nw) {
             b = u * s0;
@@ -539,11 +540,15 @@ struct TileUnits {  // tile indices fit 32 bits (the tie lists store them as u32
 // launch saturate it.  12 keeps half that rate (3 ii 10.65 -> 10.41 ms, 3 iii and config 4 ~1 %).
 // With 12-tile units a 10 % static share beat 25 % (config 2 9.77 -> 9.68 ms pipelined, 9.78 ->
 // 9.68 sequential, 3 iii 9.98 -> 9.94; 0 %: 9.72; profiles/r03/sched_static/): ~290 k grabs.
+// RC_TILE_GROUP (sched.group, rounded down to a power of two): the units come in groups of that
+// many, one global grab per group, dealt to the workgroup's waves through LDS (UnitGrab).
 constexpr uint64_t kDynChunkMin = 2;    // units of at least 2 tiles
 __host__ inline TileUnits tile_units(uint64_t n_tiles, uint64_t nw, TileSched sched) {
     TileUnits U;
     U.n_tiles = (uint32_t)n_tiles;
     U.nw = (uint32_t)nw;
+    U.gshift = 0;
+    U.n_groups = 0;
     uint64_t permille = sched.permille, chunk = sched.chunk, dyn_min = sched.dyn_min;
     if (permille > 1000) permille = 1000;
     if (chunk < kDynChunkMin) chunk = kDynChunkMin;
@@ -561,8 +566,124 @@ __host__ inline TileUnits tile_units(uint64_t n_tiles, uint64_t nw, TileSched sc
     U.chunk = (uint32_t)chunk;
     U.dyn0 = (uint32_t)(nw * U.s0);
     U.n_units = (uint32_t)(nw + (n_tiles - U.dyn0 + chunk - 1) / chunk);
+    if (sched.group) {
+        uint32_t sh = 0;
+        while ((2u << sh) <= sched.group && sh < 8) ++sh;
+        U.gshift = sh;
+        U.n_groups = (uint32_t)(((uint64_t)(U.n_units - U.nw) + (1u << sh) - 1) >> sh);
+    }
     return U;
 }
+
+// How a wave gets its next dynamic unit.
+//
+// Per-wave grabs (TileUnits.n_groups == 0, the round-3 schedule): lane 0's global atomic on the
+// one counter, issued when the wave enters a unit and read when it leaves it.  One counter hands
+// the units out in address order (the chip sweeps the bytes as one front), but it serves only
+// ~45 grabs per microsecond, so the units cannot be short: 12 tiles, ~0.1 ms of a wave, which is
+// 1 % of a config-2 launch but an eighth of the reference harness's (0.85 ms).
+//
+// Group grabs (round 5): one global grab per GROUP of 2^gshift consecutive units, dealt to the
+// workgroup's waves through LDS -- a wave takes an ordinal o from the workgroup's LDS counter;
+// o's slot k = o >> gshift is the workgroup's k-th group, sub-unit o & (2^gshift - 1).  Slot k's
+// global group index is published in s_grab_slot[k % kGrabSlots] as (k << 32 | g):
+//   * slot 0 is grabbed by thread 0 while the workgroup stages its tables (before the barrier);
+//   * the wave that takes sub-unit 0 of slot k issues the global grab for slot k + 1 -- after it
+//     has read slot k, so the workgroup's grabs return increasing values -- and publishes it when
+//     it leaves that unit (one unit later: the atomic's latency hides behind it), or at once when
+//     slot k was past the end (then slot k + 1 is too: the grabs increase);
+//   * a wave whose slot is not published yet waits on LDS (s_sleep); the publisher of slot k + 1
+//     holds slot k already and never waits before it publishes, so the waits end.
+// A wave stops at the first unit past the end; every later ordinal of its workgroup is past the
+// end too (the grabs increase), and every earlier one was taken by a wave that runs it: each
+// unit is run exactly once.  Global grabs drop by 2^gshift, so units can be short.
+constexpr uint32_t kGrabSlots = 16;
+constexpr uint32_t kGrabSpinLimit = 1u << 24;  // ~1-2 s of s_sleep waits
+__shared__ uint32_t s_grab_ord;
+__shared__ uint64_t s_grab_slot[kGrabSlots];
+
+// the tile kernel's counter buffer (256 bytes, zeroed once per workspace): word 0 the grab
+// counter (re-zeroed by the edge kernel), this word the sticky fail-safe flag of UnitGrab::next
+constexpr uint32_t kGrabErrWord = 32;
+
+template <bool kGroup>
+struct UnitGrab {
+    uint32_t v;       // lane 0: the pending global grab's result
+    uint32_t pub_k;   // the slot this wave publishes next (~0u: none)
+    bool issued;      // pub_k's global grab was issued (else it is published as past the end)
+
+    // The first global grab, issued before the workgroup stages its tables (per-wave: this
+    // wave's; group: thread 0's, for slot 0, written to LDS by seed()).
+    __device__ void start(const TileUnits &U, uint32_t *ctr) {
+        v = 0;
+        pub_k = ~0u;
+        issued = false;
+        if (U.n_units <= U.nw) return;
+        if (kGroup ? threadIdx.x == 0 : lane_id() == 0) v = atomicAdd(ctr, 1u);
+    }
+    // Group grabs: slot 0 and the ordinal counter, before the workgroup's first barrier (which
+    // makes them visible to every wave).
+    __device__ void seed(const TileUnits &U) {
+        if (!kGroup || U.n_units <= U.nw || threadIdx.x != 0) return;
+        s_grab_ord = 0;
+        s_grab_slot[0] = (uint64_t)v;  // tag 0
+        for (uint32_t i = 1; i < kGrabSlots; ++i) s_grab_slot[i] = ~0ull;
+    }
+    __device__ void publish() {
+        if (!kGroup || pub_k == ~0u) return;
+        const uint32_t g = issued ? (uint32_t)__builtin_amdgcn_readfirstlane(v) : ~0u;
+        if (lane_id() == 0)
+            __hip_atomic_store(&s_grab_slot[pub_k % kGrabSlots], ((uint64_t)pub_k << 32) | g,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        pub_k = ~0u;
+    }
+    // The wave's next dynamic unit; U.n_units or more: none left (then nothing is pending).
+    // err (may be NULL): set to 1 if a slot stayed unpublished for ~kGrabSpinLimit waits (a
+    // protocol failure: the wave then stops as if the units had run out, so the launch ends
+    // with wrong records instead of hanging the GPU; tests/test_grab_model.py models why the
+    // waits end).
+    __device__ uint32_t next(const TileUnits &U, uint32_t *ctr, uint32_t *err) {
+        if (U.n_units <= U.nw) return U.n_units;
+        if constexpr (!kGroup) {
+            const uint32_t u = U.nw + (uint32_t)__builtin_amdgcn_readfirstlane(v);
+            if (u < U.n_units && lane_id() == 0) v = atomicAdd(ctr, 1u);
+            return u;
+        }
+        publish();
+        uint32_t o = 0;
+        if (lane_id() == 0)
+            o = __hip_atomic_fetch_add(&s_grab_ord, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        o = (uint32_t)__builtin_amdgcn_readfirstlane(o);
+        const uint32_t k = o >> U.gshift, sub = o & ((1u << U.gshift) - 1);
+        uint64_t e;
+        for (uint32_t spins = 0;; ++spins) {
+            e = __hip_atomic_load(&s_grab_slot[k % kGrabSlots], __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+            e = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(e >> 32)) << 32) |
+                (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)e);
+            if ((uint32_t)(e >> 32) == k) break;
+            if (spins == kGrabSpinLimit) {  // fail-safe (never seen): stop, flag it, no hang
+                if (err && lane_id() == 0) atomicOr(err, 1u);
+                e = ~0ull;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        const uint32_t g = (uint32_t)e;
+        const bool live = g < U.n_groups;
+        if (sub == 0) {
+            pub_k = k + 1;
+            issued = live;
+            if (live && lane_id() == 0) v = atomicAdd(ctr, 1u);
+        }
+        const uint32_t u = live ? U.nw + (g << U.gshift) + sub : U.n_units;
+        if (u >= U.n_units) {
+            publish();
+            return U.n_units;
+        }
+        return u;
+    }
+};
 
 // Persistent: one 1024-thread workgroup per CU, each wave its static unit, then dynamic units.
 // G > 1: also grp[t] = the tile's group bounds (GroupRecord: the top-16 maximum of each of its
@@ -577,7 +698,7 @@ __host__ inline TileUnits tile_units(uint64_t n_tiles, uint64_t nw, TileSched sc
 //
 // The grab for a wave's next unit is issued when it enters a unit and read when it leaves it,
 // so the atomic's latency hides behind the unit's tiles.  ctr must be 0 at launch.
-template <int G>
+template <int G, bool kGroup>
 __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restrict__ tab,
                                                        StreamDesc d, uint64_t n_streams,
                                                        TileUnits U,
@@ -587,7 +708,11 @@ __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restri
                                                        uint32_t *__restrict__ xlist,
                                                        uint32_t *__restrict__ xcount,
                                                        uint32_t *__restrict__ ctr) {
-    stage_tile_tables(tab);
+    UnitGrab<kGroup> grab;
+    grab.start(U, ctr);
+    stage_tile_tables_nb(tab);
+    grab.seed(U);
+    __syncthreads();
     const uint64_t *full = reinterpret_cast<const uint64_t *>(s_tile_lds + kFullOff / 4);
     const uint64_t *tl = full, *th = full + 1024;
     const uint64_t n_tiles = U.n_tiles;
@@ -596,10 +721,6 @@ __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restri
     const uint32_t lb_a = (lane & 31) * 4, lb_b = lb_a | 0x10000u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t gw = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wave;
-    const bool dynamic = U.n_units > U.nw;
-    // the grab of the next unit: lane 0's atomic, read (readfirstlane) only when it is needed
-    uint32_t grab_v = 0;
-    if (dynamic && lane == 0) grab_v = atomicAdd(ctr, 1u);
     uint32_t u = (uint32_t)gw, ub, ue;
     U.range(u, ub, ue);
     uint32_t n_ties = 0;
@@ -620,10 +741,9 @@ __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restri
             continue;
         }
         if (lane == 0) xcount[u] = 0;
-        u = dynamic ? U.nw + (uint32_t)__builtin_amdgcn_readfirstlane(grab_v) : U.n_units;
+        u = grab.next(U, ctr, ctr + kGrabErrWord);
         if (u >= U.n_units) return;
         U.range(u, ub, ue);
-        if (lane == 0) grab_v = atomicAdd(ctr, 1u);
         t = ub;
         seek = true;
     }
@@ -662,13 +782,12 @@ __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restri
                 continue;
             }
             if (nu != u && lane == 0) xcount[nu] = 0;  // a grabbed unit without a fast tile
-            nu = dynamic ? U.nw + (uint32_t)__builtin_amdgcn_readfirstlane(grab_v) : U.n_units;
+            nu = grab.next(U, ctr, ctr + kGrabErrWord);
             if (nu >= U.n_units) {
                 nu = u;  // no more work: cur is the wave's last tile
                 break;
             }
             U.range(nu, nub, nue);
-            if (lane == 0) grab_v = atomicAdd(ctr, 1u);
             tn = nub;
             if (tn < nue) cursor.init(d, n_streams, tn);
         }
@@ -2671,6 +2790,7 @@ __device__ __forceinline__ uint64_t probe_tile(uint64_t k, uint64_t gw, uint64_t
     return (k / block * nw + gw) * block + k % block;  // the k-th tile of wave gw
 }
 
+template <bool kGroup>
 __global__ __launch_bounds__(1024) void rc_read_probe_kernel(const uint8_t *__restrict__ src,
                                                              uint64_t n_tiles,
                                                              uint32_t *__restrict__ out,
@@ -2684,17 +2804,17 @@ __global__ __launch_bounds__(1024) void rc_read_probe_kernel(const uint8_t *__re
     if (block == 0) {
         // the tile kernel's schedule (TileUnits): the static unit, then grabbed units; the next
         // tile is known one tile ahead, so the ring never drains at a unit switch
-        const bool dynamic = U.n_units > U.nw;
-        uint32_t grab_v = 0;
-        if (dynamic && lane == 0) grab_v = atomicAdd(ctr, 1u);
+        UnitGrab<kGroup> grab;
+        grab.start(U, ctr);
+        grab.seed(U);
+        __syncthreads();
         uint32_t u = (uint32_t)gw, ub, ue;
         U.range(u, ub, ue);
         auto next_unit = [&]() -> bool {  // the wave's next non-empty unit, or false
             for (;;) {
-                u = dynamic ? U.nw + (uint32_t)__builtin_amdgcn_readfirstlane(grab_v) : U.n_units;
+                u = grab.next(U, ctr, nullptr);
                 if (u >= U.n_units) return false;
                 U.range(u, ub, ue);
-                if (lane == 0) grab_v = atomicAdd(ctr, 1u);
                 if (ub < ue) return true;
             }
         };
@@ -2831,13 +2951,26 @@ int rc_launch_tiles(const KeyTables *d_tables, StreamDesc desc, uint64_t n_strea
     const TileUnits U = tile_units(n_tiles, n_waves, sched);
     // the tie lists: n_tiles slots, one count per unit; d_ctr is 0 (the edge kernel re-zeros it)
     uint32_t *d_xcount = d_xlist + n_tiles;
-    if (d_grp)
-        hipLaunchKernelGGL(rc_tile_kernel<kTileGroups>, dim3((unsigned)grid), dim3(1024), 0, st,
-                           d_tables, desc, n_streams, U, d_records, d_grp, hot, d_xlist,
+    // workgroup grabs (RC_TILE_GROUP) are a kernel of their own: the per-wave kernel keeps
+    // the round-4 code (the group protocol's registers cost the static harness 3.5 %,
+    // profiles/r05/grab/)
+    const bool grp = U.n_groups != 0;
+    if (d_grp && grp)
+        hipLaunchKernelGGL((rc_tile_kernel<kTileGroups, true>), dim3((unsigned)grid), dim3(1024), 0,
+                           st, d_tables, desc, n_streams, U, d_records, d_grp, hot, d_xlist,
                            d_xcount, d_ctr);
+    else if (d_grp)
+        hipLaunchKernelGGL((rc_tile_kernel<kTileGroups, false>), dim3((unsigned)grid), dim3(1024),
+                           0, st, d_tables, desc, n_streams, U, d_records, d_grp, hot, d_xlist,
+                           d_xcount, d_ctr);
+    else if (grp)
+        hipLaunchKernelGGL((rc_tile_kernel<1, true>), dim3((unsigned)grid), dim3(1024), 0, st,
+                           d_tables, desc, n_streams, U, d_records, d_grp, hot, d_xlist, d_xcount,
+                           d_ctr);
     else
-        hipLaunchKernelGGL(rc_tile_kernel<1>, dim3((unsigned)grid), dim3(1024), 0, st, d_tables,
-                           desc, n_streams, U, d_records, d_grp, hot, d_xlist, d_xcount, d_ctr);
+        hipLaunchKernelGGL((rc_tile_kernel<1, false>), dim3((unsigned)grid), dim3(1024), 0, st,
+                           d_tables, desc, n_streams, U, d_records, d_grp, hot, d_xlist, d_xcount,
+                           d_ctr);
     if (launch_status("rc_tile_kernel")) return 1;
     if (mid_event && hipEventRecord((hipEvent_t)mid_event, st) != hipSuccess) {
         snprintf(g_launch_err, sizeof g_launch_err, "hipEventRecord failed");
@@ -2963,22 +3096,26 @@ int rc_launch_chain(const KeyTables *d_tables, StreamDesc desc, uint64_t n_strea
 }
 
 int rc_launch_read_probe(const uint8_t *d_src, uint64_t nbytes, uint32_t *d_out, uint32_t block,
-                         void *stream) {
+                         TileSched sched, void *stream) {
     const uint64_t n_tiles = nbytes / ((uint64_t)kTileKeys * 4);
     if (n_tiles == 0) return 0;
     uint64_t grid = (n_tiles + 15) / 16;
     const uint64_t cus = (uint64_t)cu_count();
     if (grid > cus) grid = cus;
     // block (RC_PROBE_BLOCK, diagnostics): interleaved runs of tiles, static; otherwise the tile
-    // kernel's default schedule (d_out[1] is the grab counter)
-    const TileUnits U = tile_units(n_tiles, grid * (1024 / kWaveSize), TileSched{});
+    // kernel's schedule `sched` (d_out[1] is the grab counter)
+    const TileUnits U = tile_units(n_tiles, grid * (1024 / kWaveSize), sched);
     if (block == 0 && U.n_units > U.nw &&
         hipMemsetAsync(d_out + 1, 0, sizeof(uint32_t), (hipStream_t)stream) != hipSuccess) {
         snprintf(g_launch_err, sizeof g_launch_err, "hipMemsetAsync failed");
         return 1;
     }
-    hipLaunchKernelGGL(rc_read_probe_kernel, dim3((unsigned)grid), dim3(1024), 0,
-                       (hipStream_t)stream, d_src, n_tiles, d_out, (uint64_t)block, U, d_out + 1);
+    if (U.n_groups)
+        hipLaunchKernelGGL(rc_read_probe_kernel<true>, dim3((unsigned)grid), dim3(1024), 0,
+                           (hipStream_t)stream, d_src, n_tiles, d_out, (uint64_t)block, U, d_out + 1);
+    else
+        hipLaunchKernelGGL(rc_read_probe_kernel<false>, dim3((unsigned)grid), dim3(1024), 0,
+                           (hipStream_t)stream, d_src, n_tiles, d_out, (uint64_t)block, U, d_out + 1);
     return launch_status("rc_read_probe_kernel");
 }
 

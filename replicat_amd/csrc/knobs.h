@@ -36,6 +36,7 @@ enum Knob : int {
     knProbeBlock,     // RC_PROBE_BLOCK
     knGcmDebug,       // RC_GCM_DEBUG
     knTileStreams,    // RC_TILE_STREAMS
+    knTileGroup,      // RC_TILE_GROUP
     kKnobCount
 };
 
@@ -91,6 +92,9 @@ inline constexpr KnobSpec kKnobTable[kKnobCount] = {
     {"RC_TILE_STREAMS", 1, 1, 2, nullptr,
      "CU-masked tile streams of pipelined calls: 2 alternates them, so a call's tile kernel "
      "may start on CUs the previous one has left"},
+    {"RC_TILE_GROUP", 0, 0, 256, nullptr,
+     "dynamic units per workgroup grab of the tile kernel (a power of two: the workgroup's "
+     "waves take that many units from one global grab through LDS); 0: one grab per unit"},
 };
 // clang-format on
 

@@ -303,7 +303,11 @@ class _Slot:
         # §3b); 'shared': a torch stream on the process's shared queues
         self.qs = QueueStream.acquire(prod.device) if prod.queues == 'own' else None
         self.stream = self.qs.torch if self.qs is not None else torch.cuda.Stream(device=dev)
-        self.ev_cut, self.ev_upd, self.ev_done = (torch.cuda.Event() for _ in range(3))
+        # timing events when the producer records a per-batch timeline (prod.timeline)
+        tm = bool(getattr(prod, 'timeline', False))
+        self.ev_start, self.ev_up, self.ev_cut, self.ev_upd, self.ev_done = (
+            torch.cuda.Event(enable_timing=tm) for _ in range(5))
+        self.t_enqueue = 0.0
         if prod.encryption is not None:
             nb, total = prod.cipher.nonce_bytes, max(prod.cut_cap, 1)
             self.d_keys = torch.zeros((total, SLOT), dtype=torch.uint8, device=dev)
@@ -347,7 +351,8 @@ class DeviceSnapshotProducer:
                  params: Optional[bytes] = None, digest_size: int = 64,
                  batch_bytes: int = DEFAULT_BATCH, device=None, keep_contents: bool = True,
                  encryption: Optional[ChunkEncryption] = None, file_digests: str = 'auto',
-                 slots: int = 2, queues: str = 'own', read_threads: int = 4):
+                 slots: int = 2, queues: str = 'own', read_threads: int = 4,
+                 timeline: bool = False):
         import torch
         if device is None:
             device = _current_device()
@@ -364,6 +369,9 @@ class DeviceSnapshotProducer:
         # a piece of a regular file is read as up to read_threads parallel positional reads
         # (snapshot.PieceReader): the page-cache copy, not the device, bounds the producer
         self.read_threads = int(read_threads)
+        # timeline: per-batch device phases in self.profile['timeline'] (HIP timing events on
+        # the slot streams; a measurement switch)
+        self.timeline = bool(timeline)
         self.device = int(device)
         self.dev = torch.device('cuda', self.device)
         self.chunker = GpuChunker(min_length, max_length, normalize_params(params), device=self.device)
@@ -394,6 +402,7 @@ class DeviceSnapshotProducer:
             self.enc_cap, _ = self.cipher.chunks_layout(self.chunker, [self.capacity])
         # `slots` batches in flight: the host fills one while the device works on the others
         self._slots = [_Slot(self, torch) for _ in range(int(slots))]
+        self._busy = threading.Lock()  # held by the one _produce at a time
         self._look = bytearray(PIECE)  # the piece after a full batch (tells whether it is final)
 
     # ------------------------------------------------------------------- file digests
@@ -488,6 +497,18 @@ class DeviceSnapshotProducer:
         import torch
         if not self._slots:
             raise RuntimeError('DeviceSnapshotProducer is closed')
+        # one run at a time: two would fill the same slots (an abandoned stream() whose producer
+        # thread still runs -- close() it, or let its iterator go -- fails the next run here)
+        if not self._busy.acquire(blocking=False):
+            raise RuntimeError('DeviceSnapshotProducer: another run() or stream() is still '
+                               'producing on this producer (close() the ChunkStream first)')
+        try:
+            return self._produce_locked(torch, paths, read, files, zero_copy, sink, abort,
+                                        stall_timeout)
+        finally:
+            self._busy.release()
+
+    def _produce_locked(self, torch, paths, read, files, zero_copy, sink, abort, stall_timeout):
         run = _Run(self, torch, files, zero_copy, sink)
         reader = PieceReader(sort_files(paths), files, read, record=FileRecord, on_open=_fstat_size,
                              threads=self.read_threads)
@@ -495,7 +516,7 @@ class DeviceSnapshotProducer:
         # host_digest_wait: the collector thread (overlapping the next fill)
         prof = self.profile = {'fill': 0.0, 'wait_cut': 0.0, 'enqueue': 0.0, 'collect_join': 0.0,
                                'collect_wait': 0.0, 'records': 0.0, 'host_digest_wait': 0.0,
-                               'release_wait': 0.0, 'batches': 0}
+                               'release_wait': 0.0, 'batches': 0, 't0': time.perf_counter()}
         clock = time.perf_counter
         prev, look, k = None, None, 0
         # records are built on a collector thread (they copy chunk contents, holding the GIL)
@@ -603,9 +624,15 @@ class _Run:
         torch, p = self.torch, self.p
         hs = s.stream.cuda_stream
         ptr = s.dbuf.data_ptr()
+        timeline = p.timeline
+        s.t_enqueue = time.perf_counter()
         with torch.cuda.stream(s.stream):
+            if timeline:
+                s.ev_start.record(s.stream)
             if s.blen:
                 s.dbuf[:s.blen].copy_(s.host[s.off:s.off + s.blen], non_blocking=True)
+            if timeline:
+                s.ev_up.record(s.stream)
             p.chunker.chunk_device([ptr], [s.blen], [last_start], s.d_cuts.data_ptr(),
                                    s.d_count.data_ptr(), hs, open_=not s.final)
             # count and last cut end to pinned memory: the next batch's head needs them
@@ -694,6 +721,16 @@ class _Run:
                     del self.states[fi]
         t1 = clock()
         prof['collect_wait'] += t1 - t0
+        if p.timeline:
+            # one batch's device phases (HIP events on its stream) and its host latency
+            ms = lambda a, b: round(a.elapsed_time(b), 3)  # noqa: E731
+            prof.setdefault('timeline', []).append({
+                'bytes': s.blen, 'upload_ms': ms(s.ev_start, s.ev_up),
+                'chunk_ms': ms(s.ev_up, s.ev_cut), 'file_digest_ms': ms(s.ev_cut, s.ev_upd),
+                'digest_ms': ms(s.ev_upd, s.ev_done), 'device_ms': ms(s.ev_start, s.ev_done),
+                'enqueue_to_done_ms': round((t1 - s.t_enqueue) * 1e3, 3),
+                'start_at_ms': round((s.t_enqueue - prof['t0']) * 1e3, 3),
+                'collected_at_ms': round((t1 - prof['t0']) * 1e3, 3)})
         chunks, table, hnp = self.chunks, self.table, s.hnp
         zc = self.zero_copy and p.keep_contents
         # zero copy: read-only views into the pinned batch (or ciphertexts), leased per batch
@@ -748,44 +785,56 @@ class ChunkStream:
     .stream): iterate it for ``ChunkRecord``s in stream order; ``contents`` views the producer's
     pinned batch until ``release()``.  Once exhausted, ``files`` and ``chunks_table`` are the
     run's (``snapshot()`` gives the ``SnapshotStream``, records without contents).  ``close()``
-    (also on leaving a ``with`` block, or when iteration is abandoned) stops the producer."""
+    stops the producer; so does leaving a ``with`` block, abandoning the iteration (``break``:
+    the iterator's ``finally``) or dropping the stream (the producer thread holds only the queue,
+    the abort event and a result box, never the stream).  Records the consumer still holds keep
+    their batch's buffer until released (the next run waits for them)."""
 
     _END = object()
 
     def __init__(self, prod, paths, read=None, stall_timeout=None):
         import queue
         self.files: List[FileRecord] = []
-        self._q = queue.Queue()
-        self._abort = threading.Event()
-        self._run = None
+        self._q = q = queue.Queue()
+        self._abort = abort = threading.Event()
+        self._box = box = {}  # 'run': the finished _Run
         self._done = False
+        files, end = self.files, self._END
 
         def work():
             try:
-                self._run = prod._produce(paths, read, self.files, zero_copy=True,
-                                          sink=self._q.put, abort=self._abort,
-                                          stall_timeout=stall_timeout)
-                self._q.put(self._END)
+                box['run'] = prod._produce(paths, read, files, zero_copy=True, sink=q.put,
+                                           abort=abort, stall_timeout=stall_timeout)
+                q.put(end)
             except _Aborted:
-                self._q.put(self._END)
+                q.put(end)
             except BaseException as e:  # re-raised in the consumer
-                self._q.put(e)
+                q.put(e)
 
         self._thread = threading.Thread(target=work, name='rc-chunk-producer', daemon=True)
         self._thread.start()
 
+    @property
+    def _run(self):
+        return self._box.get('run')
+
     def __iter__(self):
-        while not self._done:
-            item = self._q.get()
-            if item is self._END:
-                self._done = True
-                self._thread.join()
-                return
-            if isinstance(item, BaseException):
-                self._done = True
-                self._thread.join()
-                raise item
-            yield from item
+        try:
+            while not self._done:
+                item = self._q.get()
+                if item is self._END:
+                    self._done = True
+                    self._thread.join()
+                    return
+                if isinstance(item, BaseException):
+                    self._done = True
+                    self._thread.join()
+                    raise item
+                yield from item
+                del item
+        finally:
+            if not self._done:  # abandoned: stop the producer (its queued records are dropped)
+                self.close()
 
     @property
     def chunks_table(self):

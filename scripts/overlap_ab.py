@@ -6,9 +6,9 @@ edge + chain time are printed.  Every setting must give the same cut lists.
 
     python scripts/overlap_ab.py [config] [rounds] [setting ...]   setting = seq | pR (R CUs)
                                           | pRx2 (R CUs, RC_TILE_STREAMS=2: two tile streams)
-                                          [@STATIC:CHUNK[:DYN_MIN]] (tile schedule: a chunker
-                                          created with RC_TILE_STATIC / RC_TILE_CHUNK /
-                                          RC_TILE_DYN_MIN, knobs.h)
+                                          [@STATIC:CHUNK[:DYN_MIN[:GROUP]]] (tile schedule: a
+                                          chunker created with RC_TILE_STATIC / RC_TILE_CHUNK /
+                                          RC_TILE_DYN_MIN / RC_TILE_GROUP, knobs.h)
     python scripts/overlap_ab.py 2 4 seq p8 p16 p32
 """
 import json
@@ -81,6 +81,8 @@ for s in settings:
             env.update({'RC_TILE_STATIC': parts[0], 'RC_TILE_CHUNK': parts[1]})
             if len(parts) > 2:
                 env['RC_TILE_DYN_MIN'] = parts[2]
+            if len(parts) > 3:
+                env['RC_TILE_GROUP'] = parts[3]
         if key.endswith('x2'):
             env['RC_TILE_STREAMS'] = '2'
         chunkers[key] = chunker_with(env)
@@ -122,6 +124,7 @@ for r in range(rounds):
         t, e, c, k = ch.read_kernel_timing()
         k = max(k, 1)
         res[s].append((el, t / k, (e + c) / k))
+        ch.check()  # no fail-safe stop of a group grab
         sig = (int(counts.sum().item()), int(cuts.sum().item()), int((cuts * w).sum().item()))
         if ref is None:
             ref = sig

@@ -48,6 +48,21 @@ total = sum(sizes)
 print(json.dumps({'progress': 'files written', 'bytes': total, 'files': nfiles}), flush=True)
 
 
+def phases(prod):
+    return {k: round(v, 4) for k, v in prod.profile.items() if k not in ('t0', 'timeline')}
+
+
+def timeline_of(prod):
+    """The last run's per-batch device phases (timeline=True producers), summarised."""
+    tl = prod.profile.get('timeline')
+    if not tl:
+        return {}
+    keys = ('upload_ms', 'chunk_ms', 'file_digest_ms', 'digest_ms', 'device_ms',
+            'enqueue_to_done_ms')
+    return {'timeline_median': {k: round(sorted(b[k] for b in tl)[len(tl) // 2], 3) for k in keys},
+            'timeline': tl}
+
+
 def timed(fn, reps=3):
     fn()  # warm (page cache, allocations)
     best = None
@@ -66,12 +81,15 @@ if 'parallel_reads' in DeviceSnapshotProducer.__init__.__code__.co_varnames:
 HAS_RT = 'read_threads' in DeviceSnapshotProducer.__init__.__code__.co_varnames
 if HAS_RT:  # one positional read per piece (the default reads each piece as 4 parallel parts)
     variants.insert(1, ('plain_1_reader', {'read_threads': 1}))
+plain = None
+if os.environ.get('PROBE_VARIANTS'):
+    variants = [v for v in variants if v[0] in os.environ['PROBE_VARIANTS'].split(',')]
 for name, kw in variants:
     prod = DeviceSnapshotProducer(min_length=MIN, max_length=MAX, **kw)
     dt, res = timed(lambda: prod.run(paths))
     print(json.dumps({'variant': name, 'bytes': total, 'files': nfiles, 'chunks': len(res.chunks),
                       's': round(dt, 4), 'gib_s': round(total / dt / GIB, 3),
-                      'phases_s': {k: round(v, 4) for k, v in prod.profile.items()}}), flush=True)
+                      'phases_s': phases(prod)}), flush=True)
     if name == 'plain':
         plain = res
 
@@ -118,16 +136,23 @@ if hasattr(DeviceSnapshotProducer, 'stream'):
         svars.insert(1, ('stream_release_1_reader', 0, {'read_threads': 1}))
         svars.insert(2, ('stream_release_3_slots', 0, {'slots': 3}))
         svars.insert(3, ('stream_release_2gib_batches', 0, {'batch_bytes': 2 << 30}))
+    if 'timeline' in DeviceSnapshotProducer.__init__.__code__.co_varnames:
+        svars.insert(1, ('stream_release_timeline', 0, {'timeline': True}))
+        svars.insert(2, ('stream_release_3_slots_timeline', 0, {'timeline': True, 'slots': 3}))
+    if os.environ.get('PROBE_VARIANTS'):  # a comma list: only those stream() variants
+        keep = os.environ['PROBE_VARIANTS'].split(',')
+        svars = [v for v in svars if v[0] in keep]
     for name, workers, kw in svars:
         prod = DeviceSnapshotProducer(min_length=MIN, max_length=MAX, **kw)
         dt, snap = timed(lambda: consume(prod, workers))
-        if not kw or kw.get('read_threads') or kw.get('slots') or kw.get('batch_bytes'):
+        if plain is not None and (not kw or kw.get('read_threads') or kw.get('slots')
+                                  or kw.get('batch_bytes') or kw.get('timeline')):
             assert [c.stream_end for c in snap.chunks] == [c.stream_end for c in plain.chunks]
             assert [c.digest for c in snap.chunks] == [c.digest for c in plain.chunks]
         print(json.dumps({'variant': name, 'bytes': total, 'files': nfiles,
                           'chunks': len(snap.chunks), 's': round(dt, 4),
                           'gib_s': round(total / dt / GIB, 3),
-                          'phases_s': {k: round(v, 4) for k, v in prod.profile.items()}}),
+                          'phases_s': phases(prod), **timeline_of(prod)}),
               flush=True)
 
 # CPU baseline: the oracle's chunker + hashlib over the same framed stream (one core)

@@ -42,11 +42,48 @@ def test_pmc_traffic_same_build_only(tmp_path, monkeypatch):
         'workload': 'config2', 'build_id': 'aaaa',
         'rc_tile_kernel': {'hbm_read_bytes_corrected': 64e9, 'hbm_write_bytes': 1e8}}))
     monkeypatch.setattr(bench, 'ROOT', str(tmp_path))
-    got, src = bench.pmc_traffic('2', 1024, 64 << 20, 'aaaa')
-    assert got == pytest.approx(64.1e9) and src.endswith('pmc_summary.json')
-    got, why = bench.pmc_traffic('2', 1024, 64 << 20, 'bbbb')
+    got, src = bench.pmc_traffic('config2', 'aaaa')
+    assert got == pytest.approx(64.1e9) and 'pmc_summary.json' in src
+    got, why = bench.pmc_traffic('config2', 'bbbb')
     assert got is None and 'aaaa' in why and 'bbbb' in why
-    assert bench.pmc_traffic('4', 16, 8 << 30, 'aaaa')[0] is None
+    assert bench.pmc_traffic('config4', 'aaaa')[0] is None
+    assert bench.pmc_traffic(None, 'aaaa')[0] is None
+
+
+def test_pmc_traffic_per_workload(tmp_path, monkeypatch):
+    """Round 5: one summary holds every workload; the newest round with the line's build wins."""
+    old = tmp_path / 'profiles' / 'r04'
+    new = tmp_path / 'profiles' / 'r05'
+    old.mkdir(parents=True)
+    new.mkdir(parents=True)
+    (old / 'pmc_summary.json').write_text(json.dumps({
+        'workload': 'config2', 'build_id': 'aaaa',
+        'rc_tile_kernel': {'hbm_read_bytes_corrected': 64e9}}))
+    (new / 'pmc_summary.json').write_text(json.dumps({'build_id': 'cccc', 'workloads': {
+        'harness': {'rc_tile_kernel': {'hbm_read_bytes_corrected': 5.2e9, 'hbm_write_bytes': 1e6}},
+        'config2': {'rc_tile_kernel': {'hbm_read_bytes_corrected': 65e9}}}}))
+    monkeypatch.setattr(bench, 'ROOT', str(tmp_path))
+    got, src = bench.pmc_traffic('harness', 'cccc')
+    assert got == pytest.approx(5.201e9) and src.endswith('[harness]') and 'r05' in src
+    assert bench.pmc_traffic('config2', 'cccc')[0] == pytest.approx(65e9)
+    assert bench.pmc_traffic('config2', 'aaaa')[0] == pytest.approx(64e9)  # the older build's
+    got, why = bench.pmc_traffic('harness', 'aaaa')
+    assert got is None and 'cccc' in why
+
+
+def test_workload_keys():
+    a = bench.parse(['--config', '2'])
+    assert bench.workload_key(a, 1024, 64 << 20, False, None) == 'config2'
+    a = bench.parse(['--config', '2', '--key', 'seeded'])
+    assert bench.workload_key(a, 1024, 64 << 20, False, None) == 'config2_seeded'
+    a = bench.parse(['--config', '2', '--streams', '8'])
+    assert bench.workload_key(a, 8, 64 << 20, False, None) is None
+    a = bench.parse(['--config', 'harness'])
+    assert bench.workload_key(a, 1, 5_120_000_000, False, None) == 'harness'
+    a = bench.parse(['--config', '3i'])
+    assert bench.workload_key(a, 65536, 1 << 20, False, None) is None
+    a = bench.parse(['--config', '3iii', '--min-length', '4'])
+    assert bench.workload_key(a, 65536, 1 << 20, True, None) is None
 
 
 def test_cpu_share_caps_at_the_box_share(monkeypatch):

@@ -281,3 +281,36 @@ def test_sequential_after_pipelined_shares_outputs(end):
         assert got == exp_b, rnd
     del a, b
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize('tile_streams', [1, 2])
+def test_mixed_calls_share_outputs(pipe_all, tile_streams, monkeypatch):
+    """pipelined and sequential calls alternate into ONE cuts / counts buffer (two
+    batches whose streams land in the same slots), with one and two tile streams
+    (RC_TILE_STREAMS): after every prefix of the sequence the buffer holds the last call's
+    cuts, as a sequential chunker gives them."""
+    monkeypatch.setenv('RC_TILE_STREAMS', str(tile_streams))
+    ch = GpuChunker(MIN_LENGTH, MAX_LENGTH, b'\xff' * 16)
+    n, size = 16, 16 * MIB
+    pools = []
+    for b in range(2):
+        pool = torch.empty(n * size + 64, dtype=torch.uint8, device='cuda')
+        fill_splitmix_streams(pool.data_ptr(), n, size, size, synth.DEFAULT_SEED, 800 + 300 * b, 1,
+                              _hs())
+        pools.append(pool)
+    total, caps = ch.capacity([size] * n)
+    seq = GpuChunker(MIN_LENGTH, MAX_LENGTH, b'\xff' * 16)
+    exp = [chunk_device(seq, [p[i * size:(i + 1) * size] for i in range(n)], [size] * n)
+           for p in pools]
+    assert exp[0] != exp[1]
+    cuts = torch.zeros(total, dtype=torch.int64, device='cuda')
+    counts = torch.zeros(n, dtype=torch.int64, device='cuda')
+    plan = [(0, 'p'), (1, 's'), (0, 'p'), (1, 'p'), (0, 's'), (1, 'p'), (0, 'e'), (1, 's'),
+            (0, 'p')]
+    for k in (1, 2, 3, 5, 7, 8, 9):
+        for b, how in plan[:k]:
+            ch.chunk_device(np.arange(n, dtype=np.uint64) * size + pools[b].data_ptr(), [size] * n,
+                            None, cuts.data_ptr(), counts.data_ptr(), _hs(), pipelined=how != 's',
+                            end=how == 'e')
+        ch.wait(_hs())
+        assert _ends(cuts, counts, caps) == exp[plan[k - 1][0]], plan[:k]

@@ -308,3 +308,42 @@ def test_stream_encrypted_and_abandoned(oracle, tmp_path):
                                  digest_size=32).digest()
         assert oracle.gcm_decrypt(subkey, blob[:12], blob[12:]) == \
             stream[c.stream_start:c.stream_end]
+
+
+def test_stream_abandoned_by_a_bare_loop(tmp_path):
+    """a plain ``for rec in prod.stream(p): ... break`` with no close() must
+    stop the producer thread (the iterator's finally), so that the next run() on the same
+    producer neither hangs on the old run's slots nor runs beside it; and a second run while a
+    stream is still producing fails fast instead of sharing the slots."""
+    import gc
+    import threading
+    rnd = random.Random(1505)
+    files_data = {'f%02d' % i: rnd.randbytes(rnd.randrange(200_000, 900_000)) for i in range(24)}
+    paths = write(tmp_path, files_data)
+    prod = DeviceSnapshotProducer(min_length=2_000, max_length=80_000, batch_bytes=1 << 20)
+    n = 0
+    for rec in prod.stream(paths):
+        rec.release()
+        n += 1
+        if n == 5:
+            break
+    del rec
+    gc.collect()
+    deadline = 50
+    while any(t.name == 'rc-chunk-producer' for t in threading.enumerate()) and deadline:
+        threading.Event().wait(0.1)
+        deadline -= 1
+    assert not any(t.name == 'rc-chunk-producer' for t in threading.enumerate())
+    res = prod.run(paths)
+    stream = b''.join(snapshot.stream_pieces(snapshot.sort_files(paths)))
+    assert res.chunks[-1].stream_end == len(stream)
+    assert b''.join(c.contents for c in res.chunks) == stream
+    # a stream still producing: a concurrent run() fails fast
+    st = prod.stream(paths)
+    it = iter(st)
+    first = next(it)
+    with pytest.raises(RuntimeError, match='still producing'):
+        prod.run(paths)
+    first.release()
+    st.close()
+    prod.close()

@@ -3,8 +3,12 @@ from a counter.  By default only launches of at least 128 tiles per wave (8 GiB 
 grabbed units, so the ordinary parity tests run most cases on the static path; here the same
 oracle checks run with RC_TILE_DYN_MIN=0 (every launch dynamic) and small units, so unit
 switches land everywhere: inside streams, on stream boundaries, on tiles the fast path does not
-take, on tie tiles (zeros: every tile ties), in segmented chains.  The schedule is read per
-launch (tile_units), so monkeypatch.setenv applies to the next call."""
+take, on tie tiles (zeros: every tile ties), in segmented chains.  The knobs are read when a
+chunker is created (knobs.h), and every check creates its chunkers after monkeypatch.setenv.
+Round 5: the same checks under workgroup grabs (RC_TILE_GROUP: units dealt to a workgroup's
+waves through LDS, kernels.hip UnitGrab), and rc_chunker_check after each run (no fail-safe
+stop).  Tile records come back from a poisoned buffer (rc_tile_records), so a unit that no wave
+ran shows as a wrong record."""
 import numpy as np
 import pytest
 
@@ -20,15 +24,17 @@ from gpu_util import chunk_device, device_streams  # noqa: E402
 from replicat_amd import synth  # noqa: E402
 from replicat_amd.chunker import GpuChunker  # noqa: E402
 
-SCHEDULES = [('0', '2'), ('250', '3'), ('900', '7'), ('0', '32')]
+SCHEDULES = [('0', '2', '0'), ('250', '3', '0'), ('900', '7', '0'), ('0', '32', '0'),
+             ('0', '2', '2'), ('100', '3', '32'), ('0', '2', '256'), ('500', '5', '16')]
 
 
-@pytest.fixture(params=SCHEDULES, ids=['s%s_c%s' % x for x in SCHEDULES])
+@pytest.fixture(params=SCHEDULES, ids=['s%s_c%s_g%s' % x for x in SCHEDULES])
 def dynamic(request, monkeypatch):
-    st, ck = request.param
+    st, ck, grp = request.param
     monkeypatch.setenv('RC_TILE_DYN_MIN', '0')
     monkeypatch.setenv('RC_TILE_STATIC', st)
     monkeypatch.setenv('RC_TILE_CHUNK', ck)
+    monkeypatch.setenv('RC_TILE_GROUP', grp)
     return request.param
 
 
@@ -65,6 +71,39 @@ def test_many_small_streams_dynamic(dynamic):
     got = chunk_device(ch, ts, sizes, last)
     for d, L, g in zip(datas, last, got):
         assert g == o.chunk_stream(d, mn, mx, key, L)
+
+
+@pytest.mark.parametrize('group', ['0', '32'])
+def test_harness_stream_group_schedule(monkeypatch, group):
+    """The reference harness's stream (one 5.12 GB stream, ~87 tiles per wave: static by
+    default until round 5) with every launch dynamic, per-wave and workgroup grabs of 2-tile
+    units: the cut list equals the reference's (tests/golden/harness.json)."""
+    monkeypatch.setenv('RC_TILE_DYN_MIN', '0')
+    monkeypatch.setenv('RC_TILE_STATIC', '100')
+    monkeypatch.setenv('RC_TILE_CHUNK', '2')
+    monkeypatch.setenv('RC_TILE_GROUP', group)
+    import golden_util as G
+    pieces = list(synth.harness_buffers())
+    L = sum(len(p) for p in pieces)
+    pool = torch.empty(L + 64, dtype=torch.uint8, device='cuda')
+    off = 0
+    for p in pieces:
+        pool[off:off + len(p)].copy_(torch.frombuffer(p, dtype=torch.uint8))
+        off += len(p)
+    ch = GpuChunker(128_000, 5_120_000, b'\xff' * 16)
+    total, caps = ch.capacity([L])
+    cuts = torch.zeros(total, dtype=torch.int64, device='cuda')
+    counts = torch.zeros(1, dtype=torch.int64, device='cuda')
+    for _ in range(2):  # the second call reuses the first's records buffer
+        cuts.zero_()
+        ch.chunk_device([pool.data_ptr()], [L], [L - len(pieces[-1])], cuts.data_ptr(),
+                        counts.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        ch.check()
+        k = int(counts.cpu()[0])
+        ends = cuts[:k].cpu().numpy().view(np.uint64)
+        assert G.cutlist_digest([ends]) == G.load('harness.json')['sha256']
+    del pool
+    torch.cuda.empty_cache()
 
 
 def test_constant_data_default_schedule():

@@ -1,0 +1,142 @@
+"""A model of the tile kernel's group grabs (kernels.hip UnitGrab, round 5), run under random
+interleavings on the CPU: workgroups of waves take ordinals from their LDS counter, read the
+published slot of their group, the taker of a group's first unit issues the next global grab
+(an atomic whose value arrives later, in arrival order) and publishes it when it leaves that
+unit.  Checked: every dynamic unit is run exactly once, no wave waits forever (every schedule
+drains), and each workgroup's global grabs increase.  The model follows UnitGrab.next /
+publish statement by statement; it needs no device."""
+import random
+
+import pytest
+
+SLOTS = 16  # kGrabSlots
+
+
+class Sim:
+    def __init__(self, rnd, n_wg, waves, n_units, gshift):
+        self.rnd = rnd
+        self.K = 1 << gshift
+        self.gshift = gshift
+        self.n_units = n_units
+        self.n_groups = (n_units + self.K - 1) >> gshift
+        self.ctr = 0
+        self.pending = []  # outstanding atomics: [wave, value or None]
+        self.ran = []
+        self.wgs = []
+        for w in range(n_wg):
+            # thread 0's grab for slot 0, waited for before the barrier
+            g0 = self.ctr
+            self.ctr += 1
+            wg = {'ord': 0, 'slot': {i: (None, None) for i in range(SLOTS)}, 'grabs': [g0]}
+            wg['slot'][0] = (0, g0)
+            self.wgs.append(wg)
+        self.waves = [{'wg': w, 'pub_k': None, 'issued': False, 'atom': None, 'state': 'need',
+                       'work': 0, 'k': None, 'sub': None}
+                      for w in range(n_wg) for _ in range(waves)]
+
+    def issue(self, wv):
+        a = [wv, None]
+        self.pending.append(a)
+        wv['atom'] = a
+
+    def arrive(self):
+        a = self.rnd.choice(self.pending)
+        self.pending.remove(a)
+        a[1] = self.ctr
+        self.ctr += 1
+
+    def publish(self, wv):
+        """Returns False while the wave waits for its atomic (vmcnt)."""
+        if wv['pub_k'] is None:
+            return True
+        if wv['issued']:
+            if wv['atom'][1] is None:
+                return False
+            g = wv['atom'][1]
+        else:
+            g = 1 << 32  # past the end
+        wg = self.wgs[wv['wg']]
+        k = wv['pub_k']
+        wg['slot'][k % SLOTS] = (k, g)
+        if g < (1 << 32):
+            wg['grabs'].append(g)
+        wv['pub_k'] = None
+        return True
+
+    def step(self, wv):
+        """Advance one wave by one action; False when it is blocked."""
+        st = wv['state']
+        if st == 'work':
+            wv['work'] -= 1
+            if wv['work'] <= 0:
+                wv['state'] = 'need'
+            return True
+        if st == 'need':  # next(): publish, then take an ordinal
+            if not self.publish(wv):
+                return False
+            wg = self.wgs[wv['wg']]
+            o = wg['ord']
+            wg['ord'] += 1
+            wv['k'], wv['sub'] = o >> self.gshift, o & (self.K - 1)
+            wv['state'] = 'spin'
+            return True
+        if st == 'spin':
+            wg = self.wgs[wv['wg']]
+            tag, g = wg['slot'][wv['k'] % SLOTS]
+            if tag != wv['k']:
+                assert tag is None or tag < wv['k'], 'slot overwritten before it was read'
+                return False
+            live = g < self.n_groups
+            if wv['sub'] == 0:
+                wv['pub_k'] = wv['k'] + 1
+                wv['issued'] = live
+                if live:
+                    self.issue(wv)
+            u = (g << self.gshift) + wv['sub'] if live else self.n_units
+            if u >= self.n_units:
+                wv['state'] = 'exit'
+                return True
+            self.ran.append(u)
+            wv['state'] = 'work'
+            wv['work'] = self.rnd.randint(1, 6)
+            return True
+        if st == 'exit':  # publish at once, then the wave is done
+            if not self.publish(wv):
+                return False
+            wv['state'] = 'done'
+            return True
+        return False
+
+    def run(self):
+        for _ in range(10_000_000):
+            live = [w for w in self.waves if w['state'] != 'done']
+            if not live and not self.pending:
+                return
+            moved = False
+            if self.pending and self.rnd.random() < 0.3:
+                self.arrive()
+                moved = True
+            order = self.rnd.sample(live, len(live))
+            for w in order[:self.rnd.randint(1, max(1, len(order)))]:
+                moved |= self.step(w)
+                break
+            if not moved:
+                if self.pending:
+                    self.arrive()
+                elif not any(self.step(w) for w in live):
+                    raise AssertionError('deadlock: every wave waits, no atomic in flight')
+        raise AssertionError('did not drain')
+
+
+@pytest.mark.parametrize("seed", range(200))
+def test_group_grabs_run_every_unit_once(seed):
+    rnd = random.Random(seed)
+    n_wg = rnd.choice([1, 2, 3, 7])
+    waves = rnd.choice([1, 2, 4, 16])
+    gshift = rnd.choice([0, 1, 2, 4, 5])
+    n_units = rnd.choice([0, 1, 5, 31, 32, 33, 97, 300])
+    sim = Sim(rnd, n_wg, waves, n_units, gshift)
+    sim.run()
+    assert sorted(sim.ran) == list(range(n_units))
+    for wg in sim.wgs:
+        assert wg['grabs'] == sorted(wg['grabs']), 'a workgroup\'s grabs must increase'
