@@ -193,6 +193,10 @@ int rc_fill_splitmix_at(uint8_t *d_dst, uint64_t nbytes, uint64_t seed, uint64_t
  * ceiling for the tile kernel on this device.  d_out: 4 u32 of device scratch (d_out[1] is the
  * schedule's grab counter, zeroed by the call on its stream).  Enqueue only. */
 int rc_read_probe(const uint8_t *d_src, uint64_t nbytes, uint32_t *d_out, void *hip_stream);
+/* The same probe under one chunker's tile schedule (the RC_TILE_* knobs it was created with),
+ * so that schedules can be compared in one process on one allocation (scripts/). */
+int rc_chunker_read_probe(rc_chunker *ch, const uint8_t *d_src, uint64_t nbytes, uint32_t *d_out,
+                          void *hip_stream);
 
 /* Keys j (key j covers bytes [4j-4, 4j+4)) that any argmax window of a stream (L, P) can
  * reach: the largest such j, or 0 when the stream never hashes (tail rule only). */

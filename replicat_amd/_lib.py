@@ -63,6 +63,7 @@ SIGNATURES = {
     'rc_fill_splitmix_at': (_int, [_p, _u64, _u64, _u64, _u64, _p]),
     'rc_fill_splitmix_streams': (_int, [_p, _u64, _u64, _u64, _u64, _u64, _u64, _p]),
     'rc_read_probe': (_int, [_p, _u64, _p, _p]),
+    'rc_chunker_read_probe': (_int, [_p, _p, _u64, _p, _p]),
     'rc_keys_needed': (_u64, [_u64, _u64, _u64]),
     'rc_host_key': (_u64, [_p, _u64]),
     'rc_tables_key': (_int, [_p, _u64, _p, _p, _p]),

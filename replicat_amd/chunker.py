@@ -164,6 +164,10 @@ class GpuChunker:
 
     # ---------------------------------------------------------------------- profiling
 
+    def read_probe(self, ptr, nbytes, out_ptr, stream=0):
+        """rc_read_probe under this chunker's tile schedule (its RC_TILE_* knobs)."""
+        check(lib().rc_chunker_read_probe(self._h, ptr, nbytes, out_ptr, stream or None))
+
     def timing(self, enable: bool):
         check(lib().rc_timing_enable(self._h, 1 if enable else 0))
 

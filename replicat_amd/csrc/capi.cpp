@@ -1251,6 +1251,17 @@ int rc_read_probe(const uint8_t *d_src, uint64_t nbytes, uint32_t *d_out, void *
     return RC_OK;
 }
 
+int rc_chunker_read_probe(rc_chunker *ch, const uint8_t *d_src, uint64_t nbytes, uint32_t *d_out,
+                          void *hip_stream) {
+    if (!ch) return fail(RC_ERR_ARGUMENT, "null chunker");
+    if (nbytes && (!d_src || !d_out)) return fail(RC_ERR_ARGUMENT, "null argument");
+    if (reinterpret_cast<uintptr_t>(d_src) & 15) return fail(RC_ERR_ALIGN, "source not 16-byte aligned");
+    DeviceGuard g(ch->device);
+    if (rc_launch_read_probe(d_src, nbytes, d_out, 0, ch->sched, hip_stream))
+        return fail(RC_ERR_HIP, "%s", rc_launch_error());
+    return RC_OK;
+}
+
 int rc_fill_splitmix(uint8_t *d_dst, uint64_t nbytes, uint64_t seed, uint64_t stream, void *hip_stream) {
     if (nbytes && !d_dst) return fail(RC_ERR_ARGUMENT, "null destination");
     if (rc_launch_fill(d_dst, nbytes, seed, stream, 0, hip_stream)) return fail(RC_ERR_HIP, "%s", rc_launch_error());

@@ -264,11 +264,13 @@ __device__ __forceinline__ void scan_records(const TileRecord *rec, uint64_t t_l
 // when the record's index lies inside the asked range, and otherwise as an upper bound (see
 // chain_step), both of which hold for a superset.  Only a last tile that runs past the stream's
 // final word goes to the edge kernel (it happens when jneed is within 4096 keys of the end).
-struct TileRef {
+struct TileRef {  // 24 bytes, no padding: a padded copy left two 7-byte allocas in the group-
+                  // grab kernels, which the backend promoted to LDS (14 KiB per workgroup, a
+                  // struct copy through LDS at every tile)
     const uint8_t *base;
     uint64_t j0;
-    uint64_t s;  // its stream
-    bool fast;
+    uint32_t s;     // its stream (< 2^31, checked by the host)
+    uint32_t fast;  // 0 / 1
 };
 
 // j0 + 4095 <= jmax, with jmax = (L - 4) / 4 the last key whose 8 bytes exist (adapters.cpp:73)
@@ -326,16 +328,24 @@ __device__ __forceinline__ void tile_scan(const TileRef &tr, const TileRef &nx,
     for (int it = 0; it < kTileIters; ++it) {
         // the 16 table addresses of this 16-byte slice; then the slot is free for the next
         // tile's slice (same registers: no copies when the loop wraps)
-        uint32_t a[16];
+        uint32_t a[16], r[16];
         pf_addrs(x[it].x, lb_a, lb_b, a + 0);
         pf_addrs(x[it].y, lb_a, lb_b, a + 4);
         pf_addrs(x[it].z, lb_a, lb_b, a + 8);
         pf_addrs(x[it].w, lb_a, lb_b, a + 12);
         x[it] = ring_load(nsrc, lane * 16, it);
-        const uint32_t e0 = pf_gather(a + 0);
-        const uint32_t e1 = pf_gather(a + 4);
-        const uint32_t e2 = pf_gather(a + 8);
-        const uint32_t e3 = pf_gather(a + 12);
+        // the slice's 16 lookups issued together, then folded (round 5): left to itself the
+        // scheduler gave every variant but rc_tile_kernel<1, false> a low-pressure order -- 3-4
+        // lookups, then lgkmcnt(0), ~83 full LDS drains per tile (the ISA of <4>, the small-
+        // window kernel, had it in round 4 too); the fence makes the order the same in all
+        // four kernels (16 lookups in flight, 128 VGPRs, no spills)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) r[q] = pf_lds(a[q]);
+        __builtin_amdgcn_sched_barrier(0);
+        const uint32_t e0 = __builtin_amdgcn_bitop3_b32(r[0], r[1], r[2], 0x96) ^ r[3];
+        const uint32_t e1 = __builtin_amdgcn_bitop3_b32(r[4], r[5], r[6], 0x96) ^ r[7];
+        const uint32_t e2 = __builtin_amdgcn_bitop3_b32(r[8], r[9], r[10], 0x96) ^ r[11];
+        const uint32_t e3 = __builtin_amdgcn_bitop3_b32(r[12], r[13], r[14], 0x96) ^ r[15];
         // previous word's entry for key 0 of this lane: lane-1's e3 (wave_ror:1); lane 0 takes
         // the carry = lane 63's e3 of the previous iteration (or the word before the tile).
         const uint32_t rot = __builtin_amdgcn_mov_dpp(e3, 0x13C, 0xf, 0xf, false);
@@ -445,7 +455,7 @@ struct TileCursor {
         }
         TileRef r;
         r.j0 = (t - cur) * kTileKeys;
-        r.s = s;
+        r.s = (uint32_t)s;
         if constexpr (kCache) {
             r.base = base;
             r.fast = t - cur < nfast;
@@ -577,29 +587,32 @@ __host__ inline TileUnits tile_units(uint64_t n_tiles, uint64_t nw, TileSched sc
 
 // How a wave gets its next dynamic unit.
 //
-// Per-wave grabs (TileUnits.n_groups == 0, the round-3 schedule): lane 0's global atomic on the
-// one counter, issued when the wave enters a unit and read when it leaves it.  One counter hands
-// the units out in address order (the chip sweeps the bytes as one front), but it serves only
-// ~45 grabs per microsecond, so the units cannot be short: 12 tiles, ~0.1 ms of a wave, which is
-// 1 % of a config-2 launch but an eighth of the reference harness's (0.85 ms).
+// Per-wave grabs (kGroup false, the round-3 schedule): lane 0's global atomic on the one
+// counter, issued when the wave enters a unit and read when it leaves it.  One counter hands the
+// units out in address order (the chip sweeps the bytes as one front), but it serves only ~45
+// grabs per microsecond, so the units cannot be short: 12 tiles, ~0.1 ms of a wave, which is 1 %
+// of a config-2 launch but an eighth of the reference harness's (0.85 ms).
 //
-// Group grabs (round 5): one global grab per GROUP of 2^gshift consecutive units, dealt to the
-// workgroup's waves through LDS -- a wave takes an ordinal o from the workgroup's LDS counter;
-// o's slot k = o >> gshift is the workgroup's k-th group, sub-unit o & (2^gshift - 1).  Slot k's
-// global group index is published in s_grab_slot[k % kGrabSlots] as (k << 32 | g):
+// Group grabs (kGroup, round 5): one global grab per GROUP of 2^gshift consecutive units, dealt
+// to the workgroup's waves through LDS.  A wave takes an ordinal o from the workgroup's LDS
+// counter; o's slot k = o >> gshift is the workgroup's k-th group, its sub-unit o & (2^gshift-1).
+// Slot k's global group index is published in s_grab_slot[k % kGrabSlots] as (k << 32 | g):
 //   * slot 0 is grabbed by thread 0 while the workgroup stages its tables (before the barrier);
-//   * the wave that takes sub-unit 0 of slot k issues the global grab for slot k + 1 -- after it
-//     has read slot k, so the workgroup's grabs return increasing values -- and publishes it when
-//     it leaves that unit (one unit later: the atomic's latency hides behind it), or at once when
-//     slot k was past the end (then slot k + 1 is too: the grabs increase);
-//   * a wave whose slot is not published yet waits on LDS (s_sleep); the publisher of slot k + 1
-//     holds slot k already and never waits before it publishes, so the waits end.
+//   * the wave that takes sub-unit 0 of slot k grabs slot k + 1 right after it has read slot k
+//     -- so the workgroup's grabs return increasing values -- waits for the atomic and publishes
+//     it at once (past the end: g = ~0, without a grab).  Waiting drains that wave's loads once
+//     per group; nothing is carried from unit to unit, so the tile loop keeps its registers;
+//   * a wave whose slot is not published yet waits on LDS (s_sleep) -- for the publisher of
+//     its slot, which holds the slot before it and never waits before it publishes, so the
+//     waits end (tests/test_grab_model.py runs the protocol under random interleavings).
 // A wave stops at the first unit past the end; every later ordinal of its workgroup is past the
 // end too (the grabs increase), and every earlier one was taken by a wave that runs it: each
 // unit is run exactly once.  Global grabs drop by 2^gshift, so units can be short.
 constexpr uint32_t kGrabSlots = 16;
 constexpr uint32_t kGrabSpinLimit = 1u << 24;  // ~1-2 s of s_sleep waits
 __shared__ uint32_t s_grab_ord;
+__shared__ uint32_t s_grab_cfg[2];  // gshift, n_groups: read from LDS at a switch, so the tile
+                                    // loop holds no SGPRs for them (it is at its SGPR limit)
 __shared__ uint64_t s_grab_slot[kGrabSlots];
 
 // the tile kernel's counter buffer (256 bytes, zeroed once per workspace): word 0 the grab
@@ -608,16 +621,12 @@ constexpr uint32_t kGrabErrWord = 32;
 
 template <bool kGroup>
 struct UnitGrab {
-    uint32_t v;       // lane 0: the pending global grab's result
-    uint32_t pub_k;   // the slot this wave publishes next (~0u: none)
-    bool issued;      // pub_k's global grab was issued (else it is published as past the end)
+    uint32_t v;  // per-wave grabs: lane 0's pending global grab; group: thread 0's slot-0 grab
 
     // The first global grab, issued before the workgroup stages its tables (per-wave: this
     // wave's; group: thread 0's, for slot 0, written to LDS by seed()).
     __device__ void start(const TileUnits &U, uint32_t *ctr) {
         v = 0;
-        pub_k = ~0u;
-        issued = false;
         if (U.n_units <= U.nw) return;
         if (kGroup ? threadIdx.x == 0 : lane_id() == 0) v = atomicAdd(ctr, 1u);
     }
@@ -626,22 +635,15 @@ struct UnitGrab {
     __device__ void seed(const TileUnits &U) {
         if (!kGroup || U.n_units <= U.nw || threadIdx.x != 0) return;
         s_grab_ord = 0;
+        s_grab_cfg[0] = U.gshift;
+        s_grab_cfg[1] = U.n_groups;
         s_grab_slot[0] = (uint64_t)v;  // tag 0
         for (uint32_t i = 1; i < kGrabSlots; ++i) s_grab_slot[i] = ~0ull;
     }
-    __device__ void publish() {
-        if (!kGroup || pub_k == ~0u) return;
-        const uint32_t g = issued ? (uint32_t)__builtin_amdgcn_readfirstlane(v) : ~0u;
-        if (lane_id() == 0)
-            __hip_atomic_store(&s_grab_slot[pub_k % kGrabSlots], ((uint64_t)pub_k << 32) | g,
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        pub_k = ~0u;
-    }
-    // The wave's next dynamic unit; U.n_units or more: none left (then nothing is pending).
+    // The wave's next dynamic unit; U.n_units or more: none left.
     // err (may be NULL): set to 1 if a slot stayed unpublished for ~kGrabSpinLimit waits (a
     // protocol failure: the wave then stops as if the units had run out, so the launch ends
-    // with wrong records instead of hanging the GPU; tests/test_grab_model.py models why the
-    // waits end).
+    // with wrong records instead of hanging the GPU).
     __device__ uint32_t next(const TileUnits &U, uint32_t *ctr, uint32_t *err) {
         if (U.n_units <= U.nw) return U.n_units;
         if constexpr (!kGroup) {
@@ -649,39 +651,37 @@ struct UnitGrab {
             if (u < U.n_units && lane_id() == 0) v = atomicAdd(ctr, 1u);
             return u;
         }
-        publish();
         uint32_t o = 0;
         if (lane_id() == 0)
             o = __hip_atomic_fetch_add(&s_grab_ord, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         o = (uint32_t)__builtin_amdgcn_readfirstlane(o);
-        const uint32_t k = o >> U.gshift, sub = o & ((1u << U.gshift) - 1);
-        uint64_t e;
+        const uint32_t gshift = (uint32_t)__builtin_amdgcn_readfirstlane(s_grab_cfg[0]);
+        const uint32_t n_groups = (uint32_t)__builtin_amdgcn_readfirstlane(s_grab_cfg[1]);
+        const uint32_t k = o >> gshift, sub = o & ((1u << gshift) - 1);
+        uint32_t g = ~0u;
         for (uint32_t spins = 0;; ++spins) {
-            e = __hip_atomic_load(&s_grab_slot[k % kGrabSlots], __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_WORKGROUP);
-            e = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(e >> 32)) << 32) |
-                (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)e);
-            if ((uint32_t)(e >> 32) == k) break;
+            const uint64_t e = __hip_atomic_load(&s_grab_slot[k % kGrabSlots], __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+            if ((uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(e >> 32)) == k) {
+                g = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)e);
+                break;
+            }
             if (spins == kGrabSpinLimit) {  // fail-safe (never seen): stop, flag it, no hang
                 if (err && lane_id() == 0) atomicOr(err, 1u);
-                e = ~0ull;
                 break;
             }
             __builtin_amdgcn_s_sleep(2);
         }
-        const uint32_t g = (uint32_t)e;
-        const bool live = g < U.n_groups;
-        if (sub == 0) {
-            pub_k = k + 1;
-            issued = live;
-            if (live && lane_id() == 0) v = atomicAdd(ctr, 1u);
+        const bool live = g < n_groups;
+        if (sub == 0) {  // this wave grabs and publishes slot k + 1
+            uint32_t nv = ~0u;
+            if (live && lane_id() == 0) nv = atomicAdd(ctr, 1u);
+            nv = (uint32_t)__builtin_amdgcn_readfirstlane(nv);
+            if (lane_id() == 0)
+                __hip_atomic_store(&s_grab_slot[(k + 1) % kGrabSlots], ((uint64_t)(k + 1) << 32) | nv,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
-        const uint32_t u = live ? U.nw + (g << U.gshift) + sub : U.n_units;
-        if (u >= U.n_units) {
-            publish();
-            return U.n_units;
-        }
-        return u;
+        return live ? U.nw + (g << gshift) + sub : U.n_units;
     }
 };
 

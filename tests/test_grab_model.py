@@ -1,8 +1,8 @@
 """A model of the tile kernel's group grabs (kernels.hip UnitGrab, round 5), run under random
 interleavings on the CPU: workgroups of waves take ordinals from their LDS counter, read the
-published slot of their group, the taker of a group's first unit issues the next global grab
-(an atomic whose value arrives later, in arrival order) and publishes it when it leaves that
-unit.  Checked: every dynamic unit is run exactly once, no wave waits forever (every schedule
+published slot of their group, and the taker of a group's first unit issues the next global
+grab (an atomic whose value arrives later, in arrival order), waits for it and publishes it
+before it runs its unit.  Checked: every dynamic unit is run exactly once, no wave waits forever (every schedule
 drains), and each workgroup's global grabs increase.  The model follows UnitGrab.next /
 publish statement by statement; it needs no device."""
 import random
@@ -87,16 +87,29 @@ class Sim:
                 assert tag is None or tag < wv['k'], 'slot overwritten before it was read'
                 return False
             live = g < self.n_groups
-            if wv['sub'] == 0:
+            if wv['sub'] == 0:  # grab slot k + 1 now, wait for it, publish it at once
                 wv['pub_k'] = wv['k'] + 1
                 wv['issued'] = live
                 if live:
                     self.issue(wv)
+                wv['state'] = 'publish'
+                wv['u'] = (g << self.gshift) + wv['sub'] if live else self.n_units
+                return True
             u = (g << self.gshift) + wv['sub'] if live else self.n_units
             if u >= self.n_units:
                 wv['state'] = 'exit'
                 return True
             self.ran.append(u)
+            wv['state'] = 'work'
+            wv['work'] = self.rnd.randint(1, 6)
+            return True
+        if st == 'publish':  # waits for its atomic (vmcnt), publishes, then runs its unit
+            if not self.publish(wv):
+                return False
+            if wv['u'] >= self.n_units:
+                wv['state'] = 'done'
+                return True
+            self.ran.append(wv['u'])
             wv['state'] = 'work'
             wv['work'] = self.rnd.randint(1, 6)
             return True
