@@ -66,7 +66,8 @@ def test_config2_two_ranks():
     size = mib << 20
     # value = all ranks' bytes / the slowest rank's time
     per_step = res0['ms_per_step'] / 1e3
-    assert res0["value"] == pytest.approx(2 * n * size / per_step / GIB, rel=1e-2)  # both rounded
+    # both rounded (value to 0.01 GiB/s: a loaded host makes these tiny streams ~0.2 GiB/s)
+    assert res0["value"] == pytest.approx(2 * n * size / per_step / GIB, rel=1e-2, abs=0.006)
     # kernel times are the max over ranks of the stand-in's per-call figures
     assert res0['roofline']['kernel_ms'] == pytest.approx(1.0)
     assert res0['roofline']['chain_kernel_ms'] == pytest.approx(0.2)
