@@ -19,6 +19,14 @@
 #define RC_DIAG_STREAM_AUX 2  // nt
 #endif
 
+// ---- the tile scan's 16 lookups per slice: issued together behind a scheduling fence (the
+// product), or in the compiler's own order (-DRC_DIAG_NO_SLICE_FENCE, the round-4 code)
+#ifdef RC_DIAG_NO_SLICE_FENCE
+#define RC_DIAG_SLICE_FENCE false
+#else
+#define RC_DIAG_SLICE_FENCE true
+#endif
+
 // ---- per-wave stamps of the tile kernel: s_memrealtime (100 MHz) when a wave's first tile
 // starts and when its last record is stored, and its tile count
 #ifdef RC_DIAG_TILE_STAMPS

@@ -113,11 +113,12 @@ struct ChainParams {
 // The tile kernel's work schedule (kernels.hip tile_units; knobs.h RC_TILE_STATIC / CHUNK /
 // DYN_MIN): the share of the tiles handed out statically (per mille), the dynamic unit size and
 // the tiles per wave from which a launch hands out dynamic units at all.
+// Defaults since round 5: every tile in 3-tile units, 64 units per workgroup grab (knobs.h).
 struct TileSched {
-    uint32_t permille = 100;
-    uint32_t chunk = 12;
-    uint32_t dyn_min = 128;
-    uint32_t group = 0;  // units per workgroup grab (kernels.hip UnitGrab); 0: per-wave grabs
+    uint32_t permille = 0;
+    uint32_t chunk = 3;
+    uint32_t dyn_min = 0;
+    uint32_t group = 64;  // units per workgroup grab (kernels.hip UnitGrab); 0: per-wave grabs
 };
 
 // splitmix64 finaliser (replicat_amd/synth.py)

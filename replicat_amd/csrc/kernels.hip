@@ -339,13 +339,21 @@ __device__ __forceinline__ void tile_scan(const TileRef &tr, const TileRef &nx,
         // lookups, then lgkmcnt(0), ~83 full LDS drains per tile (the ISA of <4>, the small-
         // window kernel, had it in round 4 too); the fence makes the order the same in all
         // four kernels (16 lookups in flight, 128 VGPRs, no spills)
+        uint32_t e0, e1, e2, e3;
+        if constexpr (RC_DIAG_SLICE_FENCE) {
 #pragma unroll
-        for (int q = 0; q < 16; ++q) r[q] = pf_lds(a[q]);
-        __builtin_amdgcn_sched_barrier(0);
-        const uint32_t e0 = __builtin_amdgcn_bitop3_b32(r[0], r[1], r[2], 0x96) ^ r[3];
-        const uint32_t e1 = __builtin_amdgcn_bitop3_b32(r[4], r[5], r[6], 0x96) ^ r[7];
-        const uint32_t e2 = __builtin_amdgcn_bitop3_b32(r[8], r[9], r[10], 0x96) ^ r[11];
-        const uint32_t e3 = __builtin_amdgcn_bitop3_b32(r[12], r[13], r[14], 0x96) ^ r[15];
+            for (int q = 0; q < 16; ++q) r[q] = pf_lds(a[q]);
+            __builtin_amdgcn_sched_barrier(0);
+            e0 = __builtin_amdgcn_bitop3_b32(r[0], r[1], r[2], 0x96) ^ r[3];
+            e1 = __builtin_amdgcn_bitop3_b32(r[4], r[5], r[6], 0x96) ^ r[7];
+            e2 = __builtin_amdgcn_bitop3_b32(r[8], r[9], r[10], 0x96) ^ r[11];
+            e3 = __builtin_amdgcn_bitop3_b32(r[12], r[13], r[14], 0x96) ^ r[15];
+        } else {  // the compiler's order (round 4)
+            e0 = pf_gather(a + 0);
+            e1 = pf_gather(a + 4);
+            e2 = pf_gather(a + 8);
+            e3 = pf_gather(a + 12);
+        }
         // previous word's entry for key 0 of this lane: lane-1's e3 (wave_ror:1); lane 0 takes
         // the carry = lane 63's e3 of the previous iteration (or the word before the tile).
         const uint32_t rot = __builtin_amdgcn_mov_dpp(e3, 0x13C, 0xf, 0xf, false);

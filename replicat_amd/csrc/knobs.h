@@ -70,11 +70,11 @@ inline constexpr KnobSpec kKnobTable[kKnobCount] = {
      "steps a speculative chain runs past its segment end"},
     {"RC_SEGMENT_FLOOR", 2, 1, 64, nullptr,
      "shortest automatic segment, in max_lengths"},
-    {"RC_TILE_STATIC", 100, 0, 1000, nullptr,
+    {"RC_TILE_STATIC", 0, 0, 1000, nullptr,
      "share of the tiles handed out statically, per mille (1000: fully static)"},
-    {"RC_TILE_CHUNK", 12, 2, 4096, nullptr,
+    {"RC_TILE_CHUNK", 3, 2, 4096, nullptr,
      "tiles per dynamic unit of the tile kernel"},
-    {"RC_TILE_DYN_MIN", 128, 0, int64_t(1) << 20, nullptr,
+    {"RC_TILE_DYN_MIN", 0, 0, int64_t(1) << 20, nullptr,
      "tiles per wave from which a launch hands out dynamic units"},
     {"RC_JOIN_WALK", 0, 0, 1, "0|1",
      "1: every multi-segment stream through the sequential join (comparison)"},
@@ -92,7 +92,7 @@ inline constexpr KnobSpec kKnobTable[kKnobCount] = {
     {"RC_TILE_STREAMS", 1, 1, 2, nullptr,
      "CU-masked tile streams of pipelined calls: 2 alternates them, so a call's tile kernel "
      "may start on CUs the previous one has left"},
-    {"RC_TILE_GROUP", 0, 0, 256, nullptr,
+    {"RC_TILE_GROUP", 64, 0, 256, nullptr,
      "dynamic units per workgroup grab of the tile kernel (a power of two: the workgroup's "
      "waves take that many units from one global grab through LDS); 0: one grab per unit"},
 };

@@ -15,7 +15,7 @@ torch = pytest.importorskip('torch')
 if not torch.cuda.is_available():  # pragma: no cover - CPU container
     pytest.skip('needs an MI355X', allow_module_level=True)
 
-from gpu_util import chunk_device, device_streams  # noqa: E402
+from gpu_util import chunk_device, device_streams, expected_cuts, open_prefix  # noqa: E402
 
 from replicat_amd import synth  # noqa: E402
 from replicat_amd.chunker import GpuChunker  # noqa: E402
@@ -68,19 +68,13 @@ def test_lane_chain_vs_oracle(monkeypatch, lane, mn, mx, kind):
         last.append(rnd.choice([0, 0, n, rnd.randrange(0, n + 1)]))
     ts = device_streams(sizes, datas=datas)
     got = chunk_device(ch, ts, sizes, last)
-    for d, P, g in zip(datas, last, got):
-        assert g == o.chunk_stream(d, mn, mx, key, P), (mn, mx, kind, len(d), P)
+    for d, P, g, e in zip(datas, last, got, expected_cuts(datas, mn, mx, key, last)):
+        assert g == e, (mn, mx, kind, len(d), P)
     # non-final prefixes (RC_OPEN): argmax cuts only, no tail rule
     got_open = chunk_device(ch, ts, sizes, None, open_=True)
-    for d, g in zip(datas, got_open):
-        full = o.chunk_stream(d, mn, mx, key, len(d))
-        exp, s = [], 0
-        for e in full:
-            if len(d) - s < mx:
-                break
-            exp.append(e)
-            s = e
-        assert g == exp, (mn, mx, kind, len(d))
+    fulls = expected_cuts(datas, mn, mx, key, sizes)
+    for d, g, full in zip(datas, got_open, fulls):
+        assert g == open_prefix(full, len(d), mx), (mn, mx, kind, len(d))
 
 
 def test_lane_chain_many_streams_default_switch(monkeypatch):

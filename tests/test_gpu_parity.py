@@ -13,7 +13,7 @@ torch = pytest.importorskip('torch')
 if not torch.cuda.is_available():  # pragma: no cover - CPU container
     pytest.skip('needs an MI355X', allow_module_level=True)
 
-from gpu_util import chunk_device, device_streams  # noqa: E402
+from gpu_util import chunk_device, device_streams, expected_cuts, open_prefix  # noqa: E402
 
 from replicat_amd import synth  # noqa: E402
 from replicat_amd._replicat_adapters import _gclmulchunker  # noqa: E402
@@ -187,8 +187,8 @@ def test_random_vs_oracle(seed):
         last.append(rnd.choice([0, n, rnd.randrange(0, n + 1)]))
     ts = device_streams(sizes, datas=datas)
     got = chunk_device(ch, ts, sizes, last)
-    for d, P, g in zip(datas, last, got):
-        assert g == o.chunk_stream(d, mn, mx, key, P)
+    for d, P, g, e in zip(datas, last, got, expected_cuts(datas, mn, mx, key, last)):
+        assert g == e, (mn, mx, len(d), P)
 
 
 def test_open_prefix_matches_nonfinal_calls():
@@ -362,15 +362,8 @@ def test_segmented_chains_vs_oracle(monkeypatch, seg_bytes, ext, mode):
             last.append(rnd.choice([0, n, rnd.randrange(0, n + 1)]))
         ts = device_streams(sizes, datas=datas)
         got = chunk_device(ch, ts, sizes, last)
-        for d, P, g in zip(datas, last, got):
-            assert g == o.chunk_stream(d, mn, mx, key, P), (mn, mx, len(d), P)
+        for d, P, g, e in zip(datas, last, got, expected_cuts(datas, mn, mx, key, last)):
+            assert g == e, (mn, mx, len(d), P)
         got_open = chunk_device(ch, ts, sizes, None, open_=True)
-        for d, g in zip(datas, got_open):
-            full = o.chunk_stream(d, mn, mx, key, len(d))
-            exp, s = [], 0
-            for e in full:
-                if len(d) - s < mx:
-                    break
-                exp.append(e)
-                s = e
-            assert g == exp
+        for d, g, full in zip(datas, got_open, expected_cuts(datas, mn, mx, key, sizes)):
+            assert g == open_prefix(full, len(d), mx)

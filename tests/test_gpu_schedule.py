@@ -1,13 +1,13 @@
 """The tile kernel's work schedule (kernels.hip TileUnits): static ranges, then units grabbed
-from a counter.  By default only launches of at least 128 tiles per wave (8 GiB on MI355X) use
-grabbed units, so the ordinary parity tests run most cases on the static path; here the same
-oracle checks run with RC_TILE_DYN_MIN=0 (every launch dynamic) and small units, so unit
-switches land everywhere: inside streams, on stream boundaries, on tiles the fast path does not
-take, on tie tiles (zeros: every tile ties), in segmented chains.  The knobs are read when a
-chunker is created (knobs.h), and every check creates its chunkers after monkeypatch.setenv.
-Round 5: the same checks under workgroup grabs (RC_TILE_GROUP: units dealt to a workgroup's
-waves through LDS, kernels.hip UnitGrab), and rc_chunker_check after each run (no fail-safe
-stop).  Tile records come back from a poisoned buffer (rc_tile_records), so a unit that no wave
+from a counter.  Since round 5 every launch hands out all its tiles as 3-tile units, 64 per
+workgroup grab, so the ordinary parity tests run that schedule; here the same oracle checks run
+under the older schedules (fully static, per-wave grabs) and other unit and group sizes, with
+RC_TILE_DYN_MIN=0 (every launch dynamic), so unit switches land everywhere: inside streams,
+on stream boundaries, on tiles the fast path does not take, on tie tiles (zeros: every tile
+ties), in segmented chains.  The knobs are read when a chunker is created (knobs.h), and every
+check creates its chunkers after monkeypatch.setenv.  Workgroup grabs (RC_TILE_GROUP: units
+dealt to a workgroup's waves through LDS, kernels.hip UnitGrab) are followed by
+rc_chunker_check (no fail-safe stop).  Tile records come back from a poisoned buffer (rc_tile_records), so a unit that no wave
 ran shows as a wrong record."""
 import numpy as np
 import pytest
@@ -19,12 +19,15 @@ if not torch.cuda.is_available():  # pragma: no cover - CPU container
     pytest.skip('needs an MI355X', allow_module_level=True)
 
 import test_gpu_parity as P  # noqa: E402
-from gpu_util import chunk_device, device_streams  # noqa: E402
+from gpu_util import chunk_device, device_streams, expected_cuts, open_prefix  # noqa: E402
 
 from replicat_amd import synth  # noqa: E402
 from replicat_amd.chunker import GpuChunker  # noqa: E402
 
-SCHEDULES = [('0', '2', '0'), ('250', '3', '0'), ('900', '7', '0'), ('0', '32', '0'),
+# (static per mille, unit tiles, units per workgroup grab): fully static (round 2), the round-3/4
+# per-wave grabs, small per-wave units, and workgroup grabs of 2 to 256 units (the default since
+# round 5 is 0:3:64, which every other GPU test runs)
+SCHEDULES = [('1000', '12', '0'), ('100', '12', '0'), ('0', '2', '0'), ('900', '7', '0'),
              ('0', '2', '2'), ('100', '3', '32'), ('0', '2', '256'), ('500', '5', '16')]
 
 
@@ -69,19 +72,21 @@ def test_many_small_streams_dynamic(dynamic):
     last = [int(rnd.integers(0, n + 1)) if n else 0 for n in sizes]
     ts = device_streams(sizes, datas=datas)
     got = chunk_device(ch, ts, sizes, last)
-    for d, L, g in zip(datas, last, got):
-        assert g == o.chunk_stream(d, mn, mx, key, L)
+    for g, e in zip(got, expected_cuts(datas, mn, mx, key, last)):
+        assert g == e
 
 
-@pytest.mark.parametrize('group', ['0', '32'])
-def test_harness_stream_group_schedule(monkeypatch, group):
-    """The reference harness's stream (one 5.12 GB stream, ~87 tiles per wave: static by
-    default until round 5) with every launch dynamic, per-wave and workgroup grabs of 2-tile
-    units: the cut list equals the reference's (tests/golden/harness.json)."""
-    monkeypatch.setenv('RC_TILE_DYN_MIN', '0')
-    monkeypatch.setenv('RC_TILE_STATIC', '100')
-    monkeypatch.setenv('RC_TILE_CHUNK', '2')
-    monkeypatch.setenv('RC_TILE_GROUP', group)
+@pytest.mark.parametrize('sched', ['1000:12:128:0', '100:2:0:0', '100:2:0:32'])
+def test_harness_stream_schedules(monkeypatch, sched):
+    """The reference harness's stream (one 5.12 GB stream, ~76 tiles per wave: fully static by
+    default until round 5, workgroup grabs of 3-tile units since) under the round-4 static
+    schedule, per-wave grabs and workgroup grabs of 2-tile units: the cut list equals the
+    reference's (tests/golden/harness.json)."""
+    st, ck, dm, grp = sched.split(':')
+    monkeypatch.setenv('RC_TILE_DYN_MIN', dm)
+    monkeypatch.setenv('RC_TILE_STATIC', st)
+    monkeypatch.setenv('RC_TILE_CHUNK', ck)
+    monkeypatch.setenv('RC_TILE_GROUP', grp)
     import golden_util as G
     pieces = list(synth.harness_buffers())
     L = sum(len(p) for p in pieces)
