@@ -545,9 +545,13 @@ struct TileUnits {  // tile indices fit 32 bits (the tie lists store them as u32
     }
 };
 
-// Units of a launch over n_tiles tiles by nw waves (sched: knobs.h RC_TILE_STATIC, per mille,
-// default 100: the share of the tiles handed out statically; RC_TILE_CHUNK, default 12: dynamic
-// unit size; RC_TILE_DYN_MIN, default 128: fewer tiles per wave stay fully static).  Both
+// Units of a launch over n_tiles tiles by nw waves (sched: knobs.h RC_TILE_STATIC, per mille:
+// the share of the tiles handed out statically; RC_TILE_CHUNK: dynamic unit size;
+// RC_TILE_DYN_MIN: fewer tiles per wave stay fully static; RC_TILE_GROUP: units per workgroup
+// grab).  Defaults since round 5: 0 / 3 / 0 / 64 -- every tile in 3-tile units, 64 units per
+// workgroup grab (config 2 tile kernel -3 to -4 %, the harness -5 %, 3 ii / 3 iii / config 4
+// -2 to -4 % against the round-4 schedule on one allocation each, profiles/r05/sched/).
+// Round 3/4 defaults were 100 / 12 / 128 / 0, measured so:  Both
 // measured on one allocation per config (scripts/tile_sched_ab.py, profiles/r03/sched): tile
 // kernel vs the round-2 fully static schedule, config 2 11.06 -> 9.88 ms, 3 (iii) 11.46 -> 10.32,
 // config 4 23.87 -> 21.23; the harness (76 tiles per wave) is fastest fully static.  Units were

@@ -186,6 +186,29 @@ fdt, _ = timed(file_digests_alone)
 print(json.dumps({'variant': 'hashlib_file_digests_only', 'bytes': total, 's': round(fdt, 4),
                   'gib_s': round(total / fdt / GIB, 3),
                   'largest_file_s': round(fdt * max(sizes) / total, 4)}), flush=True)
+
+
+# the same per-file BLAKE2b chains on the producer's host pool size (min(16, cpu_count) threads,
+# one file per task, 16 MiB pieces): the host's ceiling for a producer whose large files'
+# digests run on host threads (pipeline.py HOST_DIGEST_MIN)
+def file_digests_pool():
+    from concurrent.futures import ThreadPoolExecutor
+
+    def one(p):
+        with open(p, 'rb') as f:
+            h = hashlib.blake2b()
+            while piece := f.read(16 << 20):
+                h.update(piece)
+        return h.digest()
+    with ThreadPoolExecutor(max_workers=max(1, min(16, os.cpu_count() or 1))) as ex:
+        return list(ex.map(one, paths))
+
+
+if nfiles > 1:
+    pdt, _ = timed(file_digests_pool)
+    print(json.dumps({'variant': 'hashlib_file_digests_pool', 'threads': max(1, min(16, os.cpu_count() or 1)),
+                      'bytes': total, 's': round(pdt, 4), 'gib_s': round(total / pdt / GIB, 3)}),
+          flush=True)
 assert [c.stream_end for c in plain.chunks] == ends, 'cut mismatch'
 assert [c.digest for c in plain.chunks] == digs, 'digest mismatch'
 assert sorted(f.digest for f in plain.files) == sorted(fd), 'file digest mismatch'
