@@ -974,25 +974,28 @@ __global__ __launch_bounds__(256) void rc_edge_kernel(const KeyTables *__restric
     const uint64_t n_units = U.n_units;
     const uint64_t n_items = n_units + n_host;
     const uint32_t lane = lane_id();
-    // Items (tie lists of the units, then the host's tiles) are the wave's gw, gw + nw, ...,
-    // looked at 64 at a time: lane l loads item e0 + l nw's count, one ballot says which have
-    // work (round 3: ~23 units per wave on config 2 -- one dependent load each was 10 us).
-    auto needs = [&](uint64_t e0) -> uint64_t {
-        const uint64_t e = e0 + lane * nw;
+    // Items (tie lists of the units, then the host's tiles) in runs of 64: the wave takes runs
+    // gw, gw + nw, ...; lane l loads the count of item 64 c + l (one coalesced 256-byte load
+    // per run) and one ballot says which have work (round 3: ~23 units per wave on config 2 --
+    // one dependent load each was 10 us; round 5: ~1.4 M 3-tile units per config-2 launch,
+    // so the loads must be coalesced -- a lane-strided run touched 64 cache lines).
+    const uint64_t n_runs = (n_items + 63) / 64;
+    auto needs = [&](uint64_t c) -> uint64_t {
+        const uint64_t e = c * 64 + lane;
         const bool w = e < n_items && (e >= n_units || xcount[e] != 0);
         return __ballot(w);
     };
     // almost every workgroup has nothing to recompute: it leaves before staging the tables
     bool work = false;
-    for (uint64_t e0 = gw; e0 < n_items && !work; e0 += 64 * nw) work = needs(e0) != 0;
+    for (uint64_t c = gw; c < n_runs && !work; c += nw) work = needs(c) != 0;
     if (!__syncthreads_or(work)) return;
     const uint64_t *gfull = &tab->tl[0][0];
     for (uint32_t i = threadIdx.x; i < 2048u; i += blockDim.x) s_full[i] = gfull[i];
     __syncthreads();
     const uint64_t *tl = s_full, *th = s_full + 1024;
-    for (uint64_t e0 = gw; e0 < n_items; e0 += 64 * nw) {
-        for (uint64_t m = needs(e0); m; m &= m - 1) {
-            const uint64_t e = e0 + (uint64_t)__builtin_ctzll(m) * nw;
+    for (uint64_t c = gw; c < n_runs; c += nw) {
+        for (uint64_t m = needs(c); m; m &= m - 1) {
+            const uint64_t e = c * 64 + (uint64_t)__builtin_ctzll(m);
             if (e < n_units) {
                 uint32_t t0, t1;
                 U.range((uint32_t)e, t0, t1);

@@ -13,7 +13,7 @@ What it replaces, in /root/reference/replicat/repository.py:
 The stream is gathered into host batches (``batch_bytes``, pinned) exactly as the batching shim
 does (replicat_amd/adapters.py): every batch but the last is chunked as an OPEN prefix (the
 reference's non-final ``next_cut`` calls), the last with its real framing, and the uncut tail
-is carried into the next batch.  ``slots`` batches (default 2) are in flight, each on its own
+is carried into the next batch.  ``slots`` batches (default 3) are in flight, each on its own
 HIP stream with its own digest / cipher handles: the files are read straight into one pinned
 batch (``readinto``) while the device works on the others, so the BLAKE2b floor of one batch
 (its longest chunk's chain, ~55 ms for a 5.12 MB chunk) overlaps the next
@@ -26,9 +26,14 @@ from the host batch, or the device's nonce || C || T when encrypted.
 
 Memory held per producer: ``slots`` x (one pinned host batch + its HBM copy) of ``capacity`` =
 batch_bytes + max_length + 16 MiB + 128 bytes each (~1.02 GiB at the default 1 GiB batch, so ~2.1
-GiB pinned and ~2.1 GiB HBM with the default 2 slots, ~3.1 with 3); with ``encryption`` each slot
-also holds a pinned and an HBM ciphertext buffer of the same size plus 28 bytes per chunk (~4.1
-GiB pinned in all with 2 slots).  Smaller ``batch_bytes`` or ``slots`` shrink it linearly.
+GiB pinned and ~3.1 GiB HBM with the default 3 slots, ~2.1 with 2); with ``encryption`` each slot
+also holds a pinned and an HBM ciphertext buffer of the same size plus 28 bytes per chunk (~6.1
+GiB pinned in all with 3 slots).  Smaller ``batch_bytes`` or ``slots`` shrink it linearly.
+Round 5 made 3 slots the default again: with large files the producer is bound by the host's
+per-file BLAKE2b chains and page-cache copies, and with 2 slots a slot's round trip (fill, then
+~75 ms of upload + chunk digests on the device) set the pace instead -- 8 GiB in 128 files,
+15.4 GiB/s with 2 slots, 16.9 with 3, against 18.8 GiB/s for the files' digests alone on the
+same 16 host threads (profiles/r05/producer/).
 
 Two ways to consume the chunks:
 
@@ -351,7 +356,7 @@ class DeviceSnapshotProducer:
                  params: Optional[bytes] = None, digest_size: int = 64,
                  batch_bytes: int = DEFAULT_BATCH, device=None, keep_contents: bool = True,
                  encryption: Optional[ChunkEncryption] = None, file_digests: str = 'auto',
-                 slots: int = 2, queues: str = 'own', read_threads: int = 4,
+                 slots: int = 3, queues: str = 'own', read_threads: int = 4,
                  timeline: bool = False):
         import torch
         if device is None:
