@@ -127,7 +127,7 @@ def test_producer_queue_modes():
     import inspect
     sig = inspect.signature(pipeline.DeviceSnapshotProducer.__init__)
     assert sig.parameters['queues'].default == 'own'
-    assert sig.parameters['slots'].default == 2
+    assert sig.parameters['slots'].default == 3  # round 5: host-bound, 3 reach 90 % of it
     with pytest.raises(ValueError, match='queues'):
         pipeline.DeviceSnapshotProducer(queues='many', device=0)
 
