@@ -459,11 +459,15 @@ size_t records_bytes(const Plan &plan) {
 // the grab counter: allocated and zeroed once per workspace; every edge kernel leaves it 0.  A
 // launch that failed after its tile kernel was queued leaves it dirty (abandon_launch): it is
 // zeroed again on the stream of the next tile kernel, after the host has waited for the orphan.
+// The first zeroing goes on that stream too (round 5): hipMemset runs on the legacy NULL
+// stream, which a caller's non-blocking stream does not wait for, and since round 5 every
+// launch grabs its units from this counter -- a tile kernel that started before the memset had
+// landed read whatever the fresh allocation held (a GPU test saw a fresh chunker's first call
+// come back with garbage counts once).
 int ensure_ctr(Workspace &ws, hipStream_t st) {
     if (!ws.d_ctr.p) {
         if (int rc = ws.d_ctr.ensure(256)) return rc;
-        HIP_TRY(hipMemset(ws.d_ctr.p, 0, 256));
-        ws.ctr_dirty = false;
+        ws.ctr_dirty = true;
     }
     if (ws.ctr_dirty) {
         HIP_TRY(hipMemsetAsync(ws.d_ctr.p, 0, 256, st));

@@ -64,7 +64,7 @@ def pipe_all(monkeypatch):
     monkeypatch.setenv('RC_PIPE_ALL', '1')
 
 
-@pytest.mark.parametrize('reserve,force', [(8, True), (32, False), (32, True), (64, True)])
+@pytest.mark.parametrize('reserve,force', [(8, True), (32, False), (64, True)])
 def test_small_cases_pipelined(reserve, force, monkeypatch):
     """Every small case (mixed lengths and framings per stream), one pipelined call per
     parameter set.  force: on the masked streams (RC_PIPE_ALL=1), else the library's choice
