@@ -859,9 +859,24 @@ class ChunkStream:
                     item = self._q.get(timeout=0.05)
                 except Exception:
                     continue
-                del item
+                self._drop(item)
             self._thread.join()
+        # what the producer queued before it stopped: release those records now (round 5: with
+        # 3 slots a whole batch of them could sit here, holding its slot's lease, until this
+        # stream was garbage-collected -- and the next run on the producer waited for it)
+        import queue
+        while True:
+            try:
+                self._drop(self._q.get_nowait())
+            except queue.Empty:
+                break
         self._done = True
+
+    @staticmethod
+    def _drop(item):
+        if isinstance(item, list):
+            for rec in item:
+                rec.release()
 
     def __enter__(self):
         return self

@@ -172,3 +172,35 @@ def test_parallel_piece_reads_are_read_piece(tmp_path, threads):
     hooked = list(snapshot.stream_pieces(
         paths, read=lambda p: io.BytesIO(open(p, 'rb').read()), threads=threads))
     assert hooked == ref
+
+
+def test_close_releases_records_still_queued():
+    """A consumer that stops early: the records the producer thread had already queued (a whole
+    batch or more, with 3 slots) are released by close() -- not when the stream object is
+    garbage-collected -- so the next run on the producer finds its slots free (round 5: the GPU
+    test of an abandoned encrypted stream waited 60 s for such a batch's lease)."""
+    leases = [pipeline._Lease() for _ in range(3)]
+
+    def batch(lease):
+        recs = [pipeline.ChunkRecord(i + 1, i, i + 1, b'd', 0, memoryview(b'x'), lease)
+                for i in range(5)]
+        lease.take(len(recs))
+        return recs
+
+    class FakeProd:
+        def _produce(self, paths, read, files, zero_copy, sink, abort, stall_timeout=None):
+            sink(batch(leases[0]))
+            abort.wait(10)
+            # batches a collector thread hands over while the producer is already stopping: the
+            # thread is gone by the time the consumer's drain loop looks again
+            sink(batch(leases[1]))
+            sink(batch(leases[2]))
+            raise pipeline._Aborted()
+
+    with pipeline.ChunkStream(FakeProd(), []) as st:
+        for rec in st:
+            rec.release()
+            break
+        kept = st  # the stream object stays referenced, as in a `with` block
+    assert [lease.n for lease in leases] == [0, 0, 0]
+    assert kept._done
