@@ -22,7 +22,7 @@ struct GcmArgs {
     uint32_t nonce_bytes;
 };
 
-constexpr int kGcmThreads = 1024;  // 16 waves: one workgroup per CU (128 KiB of LDS)
+constexpr int kGcmThreads = 1024;  // 16 waves: one workgroup per CU (153 KiB of LDS)
 
 const char *rc_gcm_launch_error(void);
 

@@ -16,13 +16,16 @@
 // and their results Z_t form a 1024-block GHASH themselves: 32 lanes fold 32 each with H, one lane
 // folds the 32 results with H^32, adds L and multiplies by H.
 //
-// AES: T-tables in LDS.  T0 and T1 = rotl8(T0) are replicated 32x, row e (256 B) holding
-// [T0[e] x 32 | T1[e] x 32], so lane l of a ds_read_b32 half-wave always reads bank l: random
-// lookups without bank conflicts, and the address 65536 + 256 e + 4 (l mod 32) (+128 for T1) is
-// ONE v_perm_b32 of the state word and a per-lane constant (the chunker's prefilter trick,
-// kernels.hip:pf_entry).  T2 / T3 are rotl16 of T0 / T1, applied once to T0[c] ^ T1[d] ^ rot16(k)
-// (the round key pre-rotated): per round 16 v_perm + 12 VALU + 16 ds_read_b32.  Round keys are
-// expanded per chunk by one lane and then held in SGPRs.
+// AES: T-tables in LDS.  All four T_k = rotl(8k) T0 are replicated 32x in two 64 KiB regions,
+// row e (256 B) of region A holding [T0[e] x 32 | T1[e] x 32] and of region B [T2[e] x 32 |
+// T3[e] x 32], so lane l of a ds_read_b32 half-wave always reads bank l: random lookups without
+// bank conflicts, and the address 65536 R + 256 e + 4 (l mod 32) (+128 for T1 / T3) is ONE
+// v_perm_b32 of the state word and a per-lane constant (the chunker's prefilter trick,
+// kernels.hip:pf_entry): per round 16 v_perm + 8 VALU (two three-input XORs per column) + 16
+// ds_read_b32.  Until round 5 only T0 / T1 were in LDS and T2 / T3 came from one rot16 of
+// T0[c] ^ T1[d] ^ rot16(k) per column (12 VALU per round): 128 KiB of T-tables now fit because
+// the GHASH tables of H^32 and the chain results live in the AES region once the rounds are done
+// (LDS map below).  Round keys are expanded per chunk by one lane and then held in SGPRs.
 //
 // GHASH: the product by a fixed field element Y uses 32 nibble tables T[j][v] = Y . E(j, v)
 // (16 entries of 16 B per nibble position: the 16 lanes of a ds_read_b128 quarter-wave hit
@@ -59,13 +62,14 @@ typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 typedef const GLOBAL uint8_t *gcbytes;
 typedef GLOBAL uint8_t *gbytes;
 
-// LDS map (bytes)
-constexpr uint32_t kTabM = 0;        // GHASH table of M = H^1024
-constexpr uint32_t kTab32 = 8192;    // of H^32
-constexpr uint32_t kTab1 = 16384;    // of H
-constexpr uint32_t kSq = 24576;      // squaring table (constant)
-constexpr uint32_t kZ = 32768;       // 1024 chain results
-constexpr uint32_t kMisc = 49152;
+// LDS map (bytes).  The AES regions are dead once every wave has left the CTR loop (E_K(J0) is
+// computed before it): the fold's chain results and the table of H^32 reuse them then.
+constexpr uint32_t kAes = 0;          // region A: 256 rows x 256 B (T0 | T1); region B at +64 KiB (T2 | T3)
+constexpr uint32_t kZ = 0;            // after the CTR loop: 1024 chain results (16 KiB)
+constexpr uint32_t kTab32 = 16384;    // after the CTR loop: GHASH table of H^32
+constexpr uint32_t kTabM = 131072;    // GHASH table of M = H^1024
+constexpr uint32_t kTab1 = 139264;    // of H (setup for non-96-bit nonces, and the fold)
+constexpr uint32_t kMisc = 147456;
 constexpr uint32_t kRk = kMisc;      // expanded key, <= 60 words
 constexpr uint32_t kH = kMisc + 256;
 constexpr uint32_t kH32 = kMisc + 272;
@@ -73,9 +77,9 @@ constexpr uint32_t kHM = kMisc + 288;
 constexpr uint32_t kJ0 = kMisc + 304;
 constexpr uint32_t kEJ0 = kMisc + 320;
 constexpr uint32_t kP = kMisc + 512;  // 32 partial sums
-constexpr uint32_t kAes = 65536;      // 256 rows x 256 B
-constexpr uint32_t kLds = 131072;
-static_assert(kP + 512 <= kAes, "LDS map overlaps");
+constexpr uint32_t kSq = kMisc + 1024;  // squaring table (constant, setup only)
+constexpr uint32_t kLds = kSq + 8192;   // 153 KiB of the 160
+static_assert(kTab32 + 8192 <= 131072 && kTabM >= 131072 && kLds <= 163840, "LDS map overlaps");
 
 __shared__ __attribute__((aligned(16))) uint8_t s_gcm[kLds];
 
@@ -95,8 +99,8 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 
 // ------------------------------------------------------------------------------ AES
 
-// v_perm selector: byte 0 <- lo.byte0 (lane column), byte 1 <- state byte k (table row),
-// byte 2 <- lo.byte2 (= 1: the 64 KiB region at kAes), byte 3 <- 0
+// v_perm selector: byte 0 <- lo.byte0 (lane column, +128 for T1 / T3), byte 1 <- state byte k
+// (table row), byte 2 <- lo.byte2 (the region: 0 for T0 / T1, 1 for T2 / T3), byte 3 <- 0
 constexpr uint32_t sel(int k) { return 0x0C020000u | ((4u + uint32_t(k)) << 8); }
 
 __device__ __forceinline__ uint32_t tl(uint32_t w, uint32_t lo, uint32_t s) {
@@ -111,22 +115,22 @@ __device__ __forceinline__ uint32_t subword(uint32_t t) {
 }
 
 // One block.  State words are little-endian columns (byte r of word c = row r of column c), so a
-// 16-byte block loads straight into them.  rk: the schedule with the words of rounds 1..NR-1
-// stored rotated by 16 (they enter under the rot16 of T2 / T3).
+// 16-byte block loads straight into them.  lo0 .. lo3: the lane's address constants of T0 .. T3.
 template <int NR>
-__device__ __forceinline__ u32x4 aes_encrypt(u32x4 in, const uint32_t *rk, uint32_t lo0, uint32_t lo1) {
+__device__ __forceinline__ u32x4 aes_encrypt(u32x4 in, const uint32_t *rk, uint32_t lo0, uint32_t lo1,
+                                             uint32_t lo2, uint32_t lo3) {
     uint32_t s0 = in.x ^ rk[0], s1 = in.y ^ rk[1], s2 = in.z ^ rk[2], s3 = in.w ^ rk[3];
 #pragma unroll
     for (int r = 1; r < NR; ++r) {
         // column c takes row k from column c + k (ShiftRows); T_k = rotl(8k) T0 (MixColumns)
         const uint32_t n0 = xor3(tl(s0, lo0, sel(0)), tl(s1, lo1, sel(1)),
-                                 rot16(xor3(tl(s2, lo0, sel(2)), tl(s3, lo1, sel(3)), rk[4 * r])));
+                                 xor3(tl(s2, lo2, sel(2)), tl(s3, lo3, sel(3)), rk[4 * r]));
         const uint32_t n1 = xor3(tl(s1, lo0, sel(0)), tl(s2, lo1, sel(1)),
-                                 rot16(xor3(tl(s3, lo0, sel(2)), tl(s0, lo1, sel(3)), rk[4 * r + 1])));
+                                 xor3(tl(s3, lo2, sel(2)), tl(s0, lo3, sel(3)), rk[4 * r + 1]));
         const uint32_t n2 = xor3(tl(s2, lo0, sel(0)), tl(s3, lo1, sel(1)),
-                                 rot16(xor3(tl(s0, lo0, sel(2)), tl(s1, lo1, sel(3)), rk[4 * r + 2])));
+                                 xor3(tl(s0, lo2, sel(2)), tl(s1, lo3, sel(3)), rk[4 * r + 2]));
         const uint32_t n3 = xor3(tl(s3, lo0, sel(0)), tl(s0, lo1, sel(1)),
-                                 rot16(xor3(tl(s1, lo0, sel(2)), tl(s2, lo1, sel(3)), rk[4 * r + 3])));
+                                 xor3(tl(s1, lo2, sel(2)), tl(s2, lo3, sel(3)), rk[4 * r + 3]));
         s0 = n0;
         s1 = n1;
         s2 = n2;
@@ -145,8 +149,7 @@ __device__ __forceinline__ u32x4 aes_encrypt(u32x4 in, const uint32_t *rk, uint3
     return o;
 }
 
-// FIPS 197 §5.2 in little-endian words (RotWord = rotr8), one lane; the schedule goes to kRk
-// with the words of rounds 1..NR-1 rotated by 16 (see aes_encrypt).
+// FIPS 197 §5.2 in little-endian words (RotWord = rotr8), one lane; the schedule goes to kRk.
 template <int NR>
 __device__ __forceinline__ void expand_key(gcbytes key) {
     constexpr int NK = NR - 6, NW = 4 * (NR + 1);
@@ -168,16 +171,21 @@ __device__ __forceinline__ void expand_key(gcbytes key) {
         w[i] = w[i - NK] ^ t;
     }
 #pragma unroll
-    for (int i = 0; i < NW; ++i) lds<uint32_t>(kRk + 4 * i) = (i >= 4 && i < 4 * NR) ? rot16(w[i]) : w[i];
+    for (int i = 0; i < NW; ++i) lds<uint32_t>(kRk + 4 * i) = w[i];
 }
 
 // ---------------------------------------------------------------------------- GHASH
 
 // x . Y for the Y whose nibble tables sit at BASE: nibble j of x (j = 2 b: the high nibble of
 // byte b; j = 2 b + 1: the low one) with value v selects the 16 bytes at BASE + 256 j + 16 v.
+// Tables past 56 KiB (kTabM and the setup tables since round 5): a DS instruction's offset field
+// holds 16 bits, so BASE + 256 j would be OR-ed into every address by its own VALU; with BASE in
+// an opaque register each address is ONE v_and_or_b32 (nibble | BASE) and 256 j the offset.
 template <uint32_t BASE>
 __device__ __forceinline__ u32x4 tab_mul(u32x4 x) {
     u32x4 acc = {0u, 0u, 0u, 0u};
+    uint32_t base = BASE;
+    if constexpr (BASE + 32 * 256 > 65536) asm("" : "+v"(base));
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
         const uint32_t w = x[d];
@@ -185,8 +193,8 @@ __device__ __forceinline__ u32x4 tab_mul(u32x4 x) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const uint32_t j = 2 * (4 * d + k);
-            const u32x4 p = lds<u32x4>(BASE + j * 256 + ((hi >> (8 * k)) & 0xFFu));
-            const u32x4 q = lds<u32x4>(BASE + (j + 1) * 256 + ((lo >> (8 * k)) & 0xFFu));
+            const u32x4 p = lds<u32x4>((((hi >> (8 * k)) & 0xF0u) | base) + j * 256);
+            const u32x4 q = lds<u32x4>((((lo >> (8 * k)) & 0xF0u) | base) + (j + 1) * 256);
             acc = u32x4{xor3(acc.x, p.x, q.x), xor3(acc.y, p.y, q.y), xor3(acc.z, p.z, q.z),
                         xor3(acc.w, p.w, q.w)};
         }
@@ -268,15 +276,17 @@ __global__ __launch_bounds__(kGcmThreads) void rc_gcm_kernel(GcmArgs a) {
     if (a.d_total && idx >= *a.d_total) return;
     GCM_MARK(2, idx);
 
-    // constant tables
+    // constant tables: region A [T0 x 32 | T1 x 32] per row, region B [T2 x 32 | T3 x 32]
     for (int i = tid; i < 256 * 64; i += kGcmThreads) {
         const int e = i >> 6, c = i & 63;
-        const uint32_t t0 = a.te0[e];
-        lds<uint32_t>(kAes + e * 256 + c * 4) = c < 32 ? t0 : rotl8(t0);
+        const uint32_t t0 = a.te0[e], t = c < 32 ? t0 : rotl8(t0);
+        lds<uint32_t>(kAes + e * 256 + c * 4) = t;
+        lds<uint32_t>(kAes + 65536 + e * 256 + c * 4) = rot16(t);
     }
     for (int i = tid; i < 512; i += kGcmThreads)
         lds<u32x4>(kSq + i * 16) = reinterpret_cast<const u32x4 *>(a.sq)[i];
-    const uint32_t lo0 = 0x10000u | (uint32_t(lane & 31) << 2), lo1 = lo0 | 128u;
+    const uint32_t lo0 = kAes | (uint32_t(lane & 31) << 2), lo1 = lo0 | 128u;
+    const uint32_t lo2 = lo0 | 0x10000u, lo3 = lo1 | 0x10000u;
     const uint32_t nbytes = a.nonce_bytes;
     {
         const GcmItem it = a.items[idx];
@@ -299,7 +309,7 @@ __global__ __launch_bounds__(kGcmThreads) void rc_gcm_kernel(GcmArgs a) {
                 const u32x4 iv = load_bytes(nonce, 12);
                 blk = u32x4{iv.x, iv.y, iv.z, 0x01000000u};
             }
-            const u32x4 e = aes_encrypt<NR>(blk, rk, lo0, lo1);
+            const u32x4 e = aes_encrypt<NR>(blk, rk, lo0, lo1, lo2, lo3);
             if (lane == 0) {
                 lds<u32x4>(kH) = e;
                 u32x4 p = e;
@@ -317,10 +327,11 @@ __global__ __launch_bounds__(kGcmThreads) void rc_gcm_kernel(GcmArgs a) {
         __syncthreads();
 
         GCM_MARK(4, idx);
-        // ---- C: the nibble tables of H, H^32 and H^1024 (32 lanes each)
-        if (wave < 3 && lane < 32) {
-            const uint32_t src = wave == 0 ? kH : wave == 1 ? kH32 : kHM;
-            const uint32_t dst = wave == 0 ? kTab1 : wave == 1 ? kTab32 : kTabM;
+        // ---- C: the nibble tables of H and H^1024 (32 lanes each; H^32's is built after the CTR
+        // loop, in the AES region)
+        if (wave < 2 && lane < 32) {
+            const uint32_t src = wave == 0 ? kH : kHM;
+            const uint32_t dst = wave == 0 ? kTab1 : kTabM;
             build_table(dst, lds<u32x4>(src), lane);
         }
         __syncthreads();
@@ -334,7 +345,7 @@ __global__ __launch_bounds__(kGcmThreads) void rc_gcm_kernel(GcmArgs a) {
                     y = tab_mul<kTab1>(y ^ load_bytes(nonce + off, nbytes - off < 16 ? nbytes - off : 16));
                 y = tab_mul<kTab1>(y ^ u32x4{0u, 0u, 0u, bswap(nbytes * 8u)});
                 lds<u32x4>(kJ0) = y;
-                lds<u32x4>(kEJ0) = aes_encrypt<NR>(y, rk, lo0, lo1);
+                lds<u32x4>(kEJ0) = aes_encrypt<NR>(y, rk, lo0, lo1, lo2, lo3);
             }
             __syncthreads();
         }
@@ -367,7 +378,7 @@ __global__ __launch_bounds__(kGcmThreads) void rc_gcm_kernel(GcmArgs a) {
                 const u32x4 d = whole && fast ? *reinterpret_cast<const GLOBAL u32x4a4 *>(src + off)
                                               : load_bytes(src + off, n);
                 const uint32_t ctr = ctr0 + 1u + uint32_t(b);  // inc32 from J0, mod 2^32
-                const u32x4 ks = aes_encrypt<NR>(u32x4{j0x, j0y, j0z, bswap(ctr)}, rk, lo0, lo1);
+                const u32x4 ks = aes_encrypt<NR>(u32x4{j0x, j0y, j0z, bswap(ctr)}, rk, lo0, lo1, lo2, lo3);
                 const u32x4 c = keep_bytes(d ^ ks, n);
                 if (whole && fast)
                     *reinterpret_cast<GLOBAL u32x4a4 *>(dst + off) = c;
@@ -377,7 +388,9 @@ __global__ __launch_bounds__(kGcmThreads) void rc_gcm_kernel(GcmArgs a) {
             }
             acc = r == 0 ? x : (tab_mul<kTabM>(acc) ^ x);
         }
+        __syncthreads();  // every wave is past its last AES round: the T-tables are dead
         lds<u32x4>(kZ + 16 * tid) = acc;
+        if (wave == 1 && lane < 32) build_table(kTab32, lds<u32x4>(kH32), lane);
         __syncthreads();
         GCM_MARK(7, rows);
 
