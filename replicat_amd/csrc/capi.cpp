@@ -634,7 +634,16 @@ int setup_overlap(rc_chunker *ch) {
     }
     std::vector<uint32_t> tm((cus + 31) / 32, 0u), xm((cus + 31) / 32, 0u);
     for (int i = 0; i < cus; ++i) ((uint32_t)i < want ? xm : tm)[i / 32] |= 1u << (i % 32);
-    HIP_TRY(hipExtStreamCreateWithCUMask(&ch->tstream, (uint32_t)tm.size(), tm.data()));
+    // RC_TILE_MASK (measurement switch): full -- the tile stream's mask holds every CU; plain --
+    // an ordinary non-blocking stream.  Either way its workgroups may take any CU the chain
+    // kernels leave (they cannot share one: 144 KiB of LDS); dynamic units make a late one harmless
+    const int64_t tmask = ch->knobs[knTileMask];
+    if (tmask == 1)
+        for (int i = 0; i < cus; ++i) tm[i / 32] |= 1u << (i % 32);
+    if (tmask == 2)
+        HIP_TRY(hipStreamCreateWithFlags(&ch->tstream, hipStreamNonBlocking));
+    else
+        HIP_TRY(hipExtStreamCreateWithCUMask(&ch->tstream, (uint32_t)tm.size(), tm.data()));
     const hipError_t ex = hipExtStreamCreateWithCUMask(&ch->xstream, (uint32_t)xm.size(), xm.data());
     if (ex != hipSuccess) {  // both streams or neither (a call checks tstream only)
         (void)hipStreamDestroy(ch->tstream);
@@ -654,7 +663,7 @@ int setup_overlap(rc_chunker *ch) {
         if (!ch->tiled[i]) HIP_TRY(hipEventCreateWithFlags(&ch->tiled[i], hipEventDisableTiming));
     }
     ch->reserve = want;
-    ch->tile_cus = (uint32_t)cus - want;
+    ch->tile_cus = (uint32_t)cus - (tmask ? 0u : want);
     return 0;
 }
 

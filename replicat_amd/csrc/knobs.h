@@ -37,6 +37,7 @@ enum Knob : int {
     knGcmDebug,       // RC_GCM_DEBUG
     knTileStreams,    // RC_TILE_STREAMS
     knTileGroup,      // RC_TILE_GROUP
+    knTileMask,       // RC_TILE_MASK
     kKnobCount
 };
 
@@ -95,6 +96,11 @@ inline constexpr KnobSpec kKnobTable[kKnobCount] = {
     {"RC_TILE_GROUP", 64, 0, 256, nullptr,
      "dynamic units per workgroup grab of the tile kernel (a power of two: the workgroup's "
      "waves take that many units from one global grab through LDS); 0: one grab per unit"},
+    {"RC_TILE_MASK", 0, 0, 2, "masked|full|plain",
+     "tile stream of pipelined calls: masked (the CUs the chain stream does not reserve), full "
+     "(its own queue with every CU in its mask) or plain (a non-blocking stream on the shared "
+     "queues); with full / plain the tile kernel's workgroups take every CU the chain kernels "
+     "leave (measurement switch)"},
 };
 // clang-format on
 

@@ -5,6 +5,8 @@ median wall time per step over K back-to-back steps, the tile kernel's HIP-event
 edge + chain time are printed.  Every setting must give the same cut lists.
 
     python scripts/overlap_ab.py [config] [rounds] [setting ...]   setting = seq | pR (R CUs)
+                                          | mR (pipelined on R CUs, each step waits for its chain)
+                                          [+full | +plain] (RC_TILE_MASK: the tile stream's mask)
                                           | pRx2 (R CUs, RC_TILE_STREAMS=2: two tile streams)
                                           [@STATIC:CHUNK[:DYN_MIN[:GROUP]]] (tile schedule: a
                                           chunker created with RC_TILE_STATIC / RC_TILE_CHUNK /
@@ -67,7 +69,8 @@ def chunker_with(env):
 
 def chunker_key(s):
     base, _, sched = s.partition('@')
-    return sched + ('x2' if base.endswith('x2') else '')
+    base, _, mask = base.partition('+')  # p32+full / p32+plain: RC_TILE_MASK
+    return sched + ('x2' if base.endswith('x2') else '') + ('+' + mask if mask else '')
 
 
 chunkers = {}
@@ -83,8 +86,10 @@ for s in settings:
                 env['RC_TILE_DYN_MIN'] = parts[2]
             if len(parts) > 3:
                 env['RC_TILE_GROUP'] = parts[3]
-        if key.endswith('x2'):
+        if 'x2' in key:
             env['RC_TILE_STREAMS'] = '2'
+        if '+' in key:
+            env['RC_TILE_MASK'] = key.partition('+')[2]
         chunkers[key] = chunker_with(env)
 ch = next(iter(chunkers.values()))
 total, caps = ch.capacity(lens)
@@ -100,14 +105,21 @@ for r in range(rounds):
     order = settings if r % 2 == 0 else settings[::-1]
     for s in order:
         base, _, sched = s.partition('@')  # ...@STATIC:CHUNK -- the tile schedule's chunker
+        base = base.partition('+')[0]
         ch = chunkers[chunker_key(s)]
         pipe = base != 'seq'
+        # mR: pipelined on R reserved CUs, but each step waits for its own chain before the next
+        # (isolates the masked tile launch from a chain running beside it)
+        isolated = base.startswith('m')
         if pipe:
             ch.overlap(int(base[1:].split(':')[0].removesuffix('x2')))
 
         def step():
             ch.chunk_device(ptrs, lens, last, cuts.data_ptr(), counts.data_ptr(), hs,
                             pipelined=pipe)
+            if isolated:
+                ch.wait(hs)
+                torch.cuda.current_stream().synchronize()
         cuts.zero_()
         for _ in range(2):
             step()
