@@ -6,7 +6,7 @@ cd "$GRAFT_REPO_ROOT"
 out=gpurun_out/final5
 mkdir -p $out
 export TMPDIR=/tmp
-CONFIG_ARGS=("--steps 20 --calibrate --e2e" "--steps 20 --config 3iii" "--steps 20 --config 3i" "--config 4 --steps 5 --warmup 1" "--steps 20 --key seeded --cpu-streams 0" "--steps 20 --config 3ii --cpu-streams 0" "--steps 20 --config 5 --cpu-streams 0" "--steps 20 --config harness" "--steps 20 --pipeline off --cpu-streams 0")
+CONFIG_ARGS=("--steps 20 --calibrate --e2e" "--steps 20 --config 3iii" "--steps 20 --config 3i" "--config 4 --steps 5 --warmup 1" "--steps 20 --key seeded --cpu-streams 0" "--steps 20 --config 3ii --cpu-streams 0" "--steps 20 --config 5 --cpu-streams 0" "--steps 20 --config harness --calibrate" "--steps 20 --pipeline off --cpu-streams 0")
 : > $out/configs.log
 for args in "${CONFIG_ARGS[@]}"; do
   echo "== $args" | tee -a $out/configs.log

@@ -5,6 +5,8 @@ waves finish is the time a dynamic tile hand-out could recover at the end of the
     python -m replicat_amd.build --variant TSTAMPS -DRC_DIAG_TILE_STAMPS
     python scripts/tile_stamps.py [n_streams] [stream_mib] [min] [max]     (default: config 2)
     python scripts/tile_stamps.py harness                                  (the reference harness)
+    STAMPS_PIPE=32 python scripts/tile_stamps.py harness     (pipelined calls: the tile kernel on
+                                                              the CU-masked stream, 32 CUs reserved)
 """
 import ctypes
 import json
@@ -40,6 +42,9 @@ else:
     ptrs = [pool.data_ptr() + i * size for i in range(n)]
     fill_splitmix_streams(pool.data_ptr(), n, size, size, synth.DEFAULT_SEED, 0, 1, hs)
 ch = GpuChunker(mn, mx, b'\xff' * 16)
+PIPE = int(os.environ.get('STAMPS_PIPE', '0') or 0)
+if PIPE:
+    ch.overlap(PIPE)
 total, caps = ch.capacity([size] * n)
 cuts = torch.zeros(total, dtype=torch.int64, device='cuda')
 counts = torch.zeros(n, dtype=torch.int64, device='cuda')
@@ -48,7 +53,9 @@ L.rc_diag_tile_read.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
 waves = torch.cuda.get_device_properties(0).multi_processor_count * 16
 for rep in range(4):
     ch.timing(True)
-    ch.chunk_device(ptrs, [size] * n, last, cuts.data_ptr(), counts.data_ptr(), hs)
+    ch.chunk_device(ptrs, [size] * n, last, cuts.data_ptr(), counts.data_ptr(), hs,
+                    pipelined=bool(PIPE))
+    ch.wait(hs)
     torch.cuda.synchronize()
     ch.timing(False)
     tile_ms = ch.read_kernel_timing()[0]
@@ -67,7 +74,9 @@ for rep in range(4):
     q = np.percentile(ends, [0, 1, 10, 50, 90, 99, 100])
     print(json.dumps({'rep': rep, 'tile_kernel_ms': round(tile_ms, 3), 'waves': int(ok.sum()),
                       'tiles_per_wave': [int(k.min()), int(k.max())],
-                      'start_us_max': round(float(starts.max()), 1),
+                      'pipelined_reserve': PIPE,
+                      'start_us_percentiles_50_90_99_100': [round(float(x), 1) for x in
+                                                            np.percentile(starts, [50, 90, 99, 100])],
                       'end_us_percentiles_0_1_10_50_90_99_100': [round(float(x), 1) for x in q],
                       'tail_us_after_median_end': round(float(q[-1] - q[3]), 1),
                       'tail_frac_of_last_end': round(float((q[-1] - q[3]) / q[-1]), 4),

@@ -133,3 +133,25 @@ def test_constant_data_default_schedule():
         assert c[base[i]:base[i] + k[i]].tolist() == exp, i
     del pool
     torch.cuda.empty_cache()
+
+
+def test_fresh_chunkers_first_call_on_a_nonblocking_stream():
+    """Round 5: every launch grabs its units from the workspace's counter, and a NEW workspace's
+    counter was zeroed by hipMemset on the NULL stream, which a non-blocking caller stream does
+    not wait for -- a fresh chunker's first call once came back with garbage counts.  Fresh
+    chunkers, each called once from a non-blocking stream right after creation (small launches,
+    where the first tile kernel starts soonest), must all match the oracle."""
+    o = P._oracle()
+    mn, mx = 2_000, 80_000
+    sizes = [1 << 20, 3 << 20, 777_777, 5 << 20]
+    datas = [synth.stream_bytes(n, synth.DEFAULT_SEED, 60 + i) for i, n in enumerate(sizes)]
+    exp = expected_cuts(datas, mn, mx, None, [0] * len(sizes))
+    with torch.cuda.stream(torch.cuda.Stream()):
+        ts = device_streams(sizes, datas=datas)
+        for _ in range(24):
+            ch = GpuChunker(mn, mx, b'\xff' * 16)
+            assert chunk_device(ch, ts, sizes, [0] * len(sizes)) == exp
+            ch.check()
+            ch.close()
+    torch.cuda.synchronize()
+    assert o is not None
