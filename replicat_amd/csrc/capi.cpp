@@ -261,7 +261,10 @@ struct rc_chunker {
 
     // timing: events before the tile kernel, after it, after the edge kernel, after the chain
     bool timing = false;
-    std::vector<hipEvent_t> ev_pool;
+    // rc_timing_enable's per-call events: ev[0], ev[2], ev[3] only time (no system-scope fence,
+    // hipEventDisableSystemFence); ev[1] also hands the tile kernel's records to the chain
+    // stream in pipelined calls, so it is an ordinary event (ev_pool_sync)
+    std::vector<hipEvent_t> ev_pool, ev_pool_sync;
     std::vector<std::array<hipEvent_t, 4>> ev_rec;
 };
 
@@ -545,12 +548,17 @@ int upload_and_launch(rc_chunker *ch, Workspace &ws, const Plan &plan, ChainPara
     const StreamDesc d = desc_view(ws.d_desc.p, plan.n);
     std::array<hipEvent_t, 4> ev{};
     if (ch->timing) {
-        for (auto &e : ev) {
-            if (ch->ev_pool.empty()) {
-                HIP_TRY(hipEventCreate(&e));
+        // round 5: timing events with the default system-scope fence cost a harness step
+        // ~20 us (0.808 vs 0.829 ms per step with and without them on one box,
+        // profiles/r05/warmup/ab_harness*.log)
+        for (int k = 0; k < 4; ++k) {
+            std::vector<hipEvent_t> &pool = k == 1 ? ch->ev_pool_sync : ch->ev_pool;
+            if (pool.empty()) {
+                HIP_TRY(k == 1 ? hipEventCreate(&ev[k])
+                               : hipEventCreateWithFlags(&ev[k], hipEventDisableSystemFence));
             } else {
-                e = ch->ev_pool.back();
-                ch->ev_pool.pop_back();
+                ev[k] = pool.back();
+                pool.pop_back();
             }
         }
         HIP_TRY(hipEventRecord(ev[0], ts));
@@ -839,6 +847,7 @@ void rc_chunker_destroy(rc_chunker *ch) {
         for (auto &r : ch->ev_rec)
             for (auto e : r) (void)hipEventDestroy(e);
         for (auto e : ch->ev_pool) (void)hipEventDestroy(e);
+        for (auto e : ch->ev_pool_sync) (void)hipEventDestroy(e);
     }
     delete ch;
 }
@@ -1231,7 +1240,7 @@ int rc_timing_read_kernels(rc_chunker *ch, double *tile_ms, double *edge_ms, dou
             HIP_TRY(hipEventElapsedTime(&x, r[k], r[k + 1]));
             t[k] += x;
         }
-        for (auto e : r) ch->ev_pool.push_back(e);
+        for (int k = 0; k < 4; ++k) (k == 1 ? ch->ev_pool_sync : ch->ev_pool).push_back(r[k]);
     }
     if (tile_ms) *tile_ms = t[0];
     if (edge_ms) *edge_ms = t[1];

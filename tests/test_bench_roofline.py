@@ -92,3 +92,16 @@ def test_cpu_share_caps_at_the_box_share(monkeypatch):
     assert bench.cpu_share() == (16, 256)
     monkeypatch.delenv('OMP_NUM_THREADS')
     assert bench.cpu_share() == (256, 256)
+
+
+def test_default_warmup_per_config():
+    """2 warm-up steps by default (the driver's contract), 50 for the sub-millisecond
+    configurations (the harness, 3 i: the GPU clock still ramps after the host-side setup);
+    an explicit --warmup is always honoured."""
+    import bench
+    assert bench.parse([]).warmup == 2
+    assert bench.parse(['--config', '3iii']).warmup == 2
+    assert bench.parse(['--config', 'harness']).warmup == bench.WARMUP_SHORT == 50
+    assert bench.parse(['--config', '3i']).warmup == 50
+    assert bench.parse(['--config', 'harness', '--warmup', '3']).warmup == 3
+    assert bench.parse(['--warmup', '0']).warmup == 0
