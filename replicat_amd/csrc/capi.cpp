@@ -663,7 +663,9 @@ int setup_overlap(rc_chunker *ch) {
     // workgroups: its workgroups take the CUs the previous launch leaves (their workspaces are
     // distinct; a call's chain still follows its own tile kernel and the previous chain)
     if (ch->knobs[knTileStreams] == 2 &&
-        hipExtStreamCreateWithCUMask(&ch->tstream2, (uint32_t)tm.size(), tm.data()) != hipSuccess)
+        (tmask == 2 ? hipStreamCreateWithFlags(&ch->tstream2, hipStreamNonBlocking)
+                    : hipExtStreamCreateWithCUMask(&ch->tstream2, (uint32_t)tm.size(), tm.data())) !=
+            hipSuccess)
         ch->tstream2 = nullptr;  // one tile stream: still correct
     if (!ch->fstream) HIP_TRY(hipStreamCreateWithFlags(&ch->fstream, hipStreamNonBlocking));
     for (int i = 0; i < 2; ++i) {
