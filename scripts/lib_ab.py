@@ -6,6 +6,10 @@ comparison.  Every build must produce the same cut lists (except the RC_DIAG_NO_
 diagnostic build, diag/lib_NOTAIL.so, which stores no records and is timed only).
 
     python scripts/lib_ab.py [config] [rounds] LIB [LIB ...]      config: 2 | 3ii | 3iii | 4 | harness
+
+LIB_AB_FLAGS (environment): the rc_chunk_device flags of every call (2 = RC_PIPELINED; with
+RC_PIPE_ALL=1 small-window batches overlap too).  Timing-only builds whose cut lists differ by
+design carry NOTAIL, NOEXACT or NOWORDS in their file name.
 """
 import ctypes
 import json
@@ -23,6 +27,7 @@ from replicat_amd.chunker import fill_splitmix_streams  # noqa: E402
 cfg = sys.argv[1] if len(sys.argv) > 1 else '2'
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 6
 paths = sys.argv[3:] or [_lib.LIB_PATH]
+FLAGS = int(os.environ.get('LIB_AB_FLAGS', '0'))
 
 
 def load(path):
@@ -76,7 +81,7 @@ for r in range(rounds):
     for p, L, h, _ in order:
         def call():
             rc = L.rc_chunk_device(h, len(lens), ptrs.ctypes.data, lens.ctypes.data,
-                                   last.ctypes.data, 0, cuts.data_ptr(), counts.data_ptr(), hs)
+                                   last.ctypes.data, FLAGS, cuts.data_ptr(), counts.data_ptr(), hs)
             assert rc == 0, L.rc_last_error()
         cuts.zero_()  # a diagnostic build's longer lists must not leave entries behind
         for _ in range(2):
@@ -92,7 +97,7 @@ for r in range(rounds):
         L.rc_timing_read_kernels(h, ctypes.byref(t), ctypes.byref(e), ctypes.byref(c), ctypes.byref(k))
         res[p].append((t.value / k.value, e.value / k.value, c.value / k.value))
         sig = (int(counts.sum().item()), int(cuts.sum().item()))
-        if 'NOTAIL' not in p and 'NOEXACT' not in p:  # diagnostic builds without exact records
+        if not any(t in p for t in ('NOTAIL', 'NOEXACT', 'NOWORDS')):  # timing-only builds
             ref = ref or sig
             assert sig == ref, (p, sig, ref)
 out = {'config': cfg, 'rounds': rounds}
