@@ -37,6 +37,15 @@ extern "C" {
 #define RC_ERR_HIP 12       /* a HIP runtime call failed (message in rc_last_error)             */
 #define RC_ERR_OVERFLOW 13  /* a stream produced more cuts than its capacity (never expected)   */
 #define RC_ERR_NO_DEVICE 14 /* no usable gfx950 device                                          */
+#define RC_ERR_DEVICE_FAULT 15 /* the tile kernel took its fail-safe stop (a workgroup grab never
+                              published, kernels.hip UnitGrab): that call's cuts are not the
+                              reference's and were not returned (never observed)               */
+
+/* Per-stream counts written by rc_chunk_device besides the cut count itself */
+#define RC_COUNT_OVERFLOW (-1) /* the stream produced more cuts than its capacity (never expected) */
+#define RC_COUNT_FAULT (-3)    /* the call's tile kernel took its fail-safe stop: EVERY stream of
+                                  the call gets this count and none of its cuts is valid
+                                  (RC_ERR_DEVICE_FAULT on the blocking paths)                    */
 
 /* rc_chunk_* flags */
 #define RC_OPEN 1u /* every stream is an OPEN prefix: its bytes all belong to non-final pieces, so
@@ -108,7 +117,9 @@ uint64_t rc_cut_capacity(const rc_chunker *ch, uint64_t n, const uint64_t *lens,
  *   last_piece[i] = P_i, start of the stream's last piece (0 = one piece; P_i <= L_i).
  * Writes stream i's chunk END offsets (u64, relative to the stream) to
  * d_cuts[cut_base[i] ..] where cut_base = exclusive prefix sum of the capacities of
- * rc_cut_capacity, and the count to d_counts[i] (int64; -1 = capacity overflow).
+ * rc_cut_capacity, and the count to d_counts[i] (int64; RC_COUNT_OVERFLOW = capacity overflow,
+ * RC_COUNT_FAULT = the call's tile kernel took its fail-safe stop -- every count of the call is
+ * then RC_COUNT_FAULT: a caller that reads the counts must treat any negative one as an error).
  * The host arrays are read before return; the work is enqueued on `hip_stream` (a
  * hipStream_t, NULL = default stream) and the call returns without synchronising.  With
  * RC_PIPELINED the kernels go to the chunker's own streams instead (see the flag). */
@@ -155,11 +166,13 @@ int rc_chunk_host(rc_chunker *ch, uint64_t n, const uint8_t *const *streams,
                   const uint64_t *lens, const uint64_t *last_piece, uint32_t flags,
                   uint64_t *cuts, int64_t *counts);
 
-/* Waits for the chunker's calls so far and reports a tile-kernel fail-safe stop: with
+/* Waits for the chunker's calls so far and reports tile-kernel fail-safe stops: with
  * workgroup grabs (RC_TILE_GROUP) a wave that waited ~1 s for its group's grab to be published
- * stops rather than hang the GPU, leaving that launch's records incomplete.  RC_OK, or
- * RC_ERR_HIP with rc_last_error() naming it.  (Never observed; the tests call it after every
- * dynamic-schedule run.)  Not a reference interface: replicat has no device. */
+ * stops rather than hang the GPU, leaving that launch's records incomplete (its counts are then
+ * RC_COUNT_FAULT, and rc_next_cut / rc_chunk_host fail with RC_ERR_DEVICE_FAULT).  RC_OK, or
+ * RC_ERR_DEVICE_FAULT with rc_last_error() giving how many calls faulted since the previous
+ * check; the count restarts at every check.  (Never observed outside the diagnostic build that
+ * forces it, diag/lib_GRABFAULT.so.)  Not a reference interface: replicat has no device. */
 int rc_chunker_check(rc_chunker *ch);
 
 /* Kernel timing, for bench.py's roofline: while enabled, every rc_chunk_device call records

@@ -26,6 +26,9 @@ RC_ERR_ALIGN = 11
 RC_ERR_HIP = 12
 RC_ERR_OVERFLOW = 13
 RC_ERR_NO_DEVICE = 14
+RC_ERR_DEVICE_FAULT = 15
+RC_COUNT_OVERFLOW = -1  # rc_chunk_device's per-stream counts besides the cut count
+RC_COUNT_FAULT = -3
 RC_OPEN = 1
 RC_PIPELINED = 2
 RC_PIPELINE_END = 4
@@ -110,6 +113,25 @@ class ChunkerError(RuntimeError):
         self.code = code
 
 
+class ChunkerFault(ChunkerError):
+    """The tile kernel took its fail-safe stop (RC_ERR_DEVICE_FAULT, RC_COUNT_FAULT): the call's
+    cuts are not the reference's and must not be used."""
+
+
+def check_counts(counts):
+    """Raise for the negative per-stream counts of rc_chunk_device (any int sequence or array
+    read back from the device): ChunkerFault for RC_COUNT_FAULT, ChunkerError(RC_ERR_OVERFLOW)
+    for anything else below 0.  Every reader of device counts calls it before using a cut."""
+    import numpy as np
+    c = np.asarray(counts).reshape(-1)
+    if c.size == 0 or int(c.min()) >= 0:
+        return
+    if (c == RC_COUNT_FAULT).any():
+        raise ChunkerFault(RC_ERR_DEVICE_FAULT, 'tile kernel fail-safe stop: a workgroup grab was '
+                           'never published, so the call\'s cuts are not the reference\'s')
+    raise ChunkerError(RC_ERR_OVERFLOW, f'stream {int(np.argmax(c < 0))} overflowed its cut capacity')
+
+
 _lock = threading.Lock()
 _lib = None
 
@@ -152,4 +174,6 @@ def check(code):
         raise ValueError(msg)
     if code == RC_ERR_NO_DEVICE:
         raise ChunkerUnavailable(msg)
+    if code == RC_ERR_DEVICE_FAULT:
+        raise ChunkerFault(code, msg)
     raise ChunkerError(code, msg)

@@ -16,7 +16,8 @@ import threading
 import numpy as np
 
 from . import _lib
-from ._lib import RC_OPEN, RC_PIPELINE_END, RC_PIPELINED, check, lib
+from ._lib import (RC_OPEN, RC_PIPELINE_END, RC_PIPELINED, ChunkerError, ChunkerFault, check,
+                   check_counts, lib)
 
 MIN_LENGTH = 128_000     # replicat/utils/adapters.py:259
 MAX_LENGTH = 5_120_000   # replicat/utils/adapters.py:260
@@ -89,7 +90,11 @@ class GpuChunker:
         streams, this call's chain beside the next call's tile kernel; ``stream`` orders the
         inputs only, and ``wait(stream)`` orders the outputs.  Keep the input and output
         tensors alive until then: torch's caching allocator sees only ``stream``.  ``end``
-        (RC_PIPELINE_END): the end of a pipelined sequence -- the chain runs on every CU."""
+        (RC_PIPELINE_END): the end of a pipelined sequence -- the chain runs on every CU.
+
+        The counts are the call's error report: read them back through ``check_counts`` (or
+        ``counts_host``) before using a cut -- a negative count is a capacity overflow or, for
+        every stream of the call, RC_COUNT_FAULT (the tile kernel's fail-safe stop)."""
         ptrs, lens = _ptr_array(ptrs), _ptr_array(lens)
         last = _ptr_array(last_piece if last_piece is not None else np.zeros(len(lens)))
         flags = ((RC_OPEN if open_ else 0) | (RC_PIPELINED if pipelined else 0)
@@ -113,8 +118,9 @@ class GpuChunker:
         return int(lib().rc_chunker_pipelined_calls(self._h))
 
     def check(self):
-        """Wait for every call so far and raise if a tile kernel took its fail-safe stop (a
-        workgroup grab never published: rc_chunker_check)."""
+        """Wait for every call so far and raise ChunkerFault if any call since the last check
+        took the tile kernel's fail-safe stop (a workgroup grab never published:
+        rc_chunker_check)."""
         check(lib().rc_chunker_check(self._h))
 
     def wait(self, stream=0):
@@ -199,12 +205,13 @@ class QueueStream:
     Take streams from the process-wide pool (``QueueStream.acquire`` / ``release``): pooled
     streams are reused, never destroyed while the process runs, and released by the library's
     exit hook after Python's own finalisation.  ``close()`` destroys a stream at once only if
-    torch never wrapped it (``torch`` never taken); a wrapped stream is retired instead -- out of
-    the pool, never handed out again, destroyed by the exit hook like the pooled ones
+    torch never wrapped it (``torch`` never taken); a wrapped stream goes back to the pool under
+    a fresh wrapper instead (safe to reuse, not to destroy: the next ``acquire`` hands it out, and
+    the exit hook destroys it like the other pooled ones), so closing wrapped streams in a loop
+    keeps at most as many streams -- and hardware queues -- as were ever in use at once
     (INTEGRATION §7)."""
 
     _pool = {}
-    _retired = []  # closed streams torch has seen: kept until the library's exit hook
     _lock = threading.Lock()
 
     def __init__(self, device=None):
@@ -249,15 +256,19 @@ class QueueStream:
         return self._torch
 
     def close(self):
-        """Done with the stream for good.  Destroyed now if torch never wrapped it; otherwise
-        retired (torch may still record an event on it when it frees a tensor used there)."""
+        """Done with this object for good.  The stream is destroyed now if torch never wrapped
+        it; otherwise (torch may still record an event on it when it frees a tensor used there)
+        it returns to the pool under a fresh wrapper, and this object is closed."""
         with QueueStream._lock:
             if self._pooled:
                 QueueStream._pool[self.device].remove(self)
                 self._pooled = False
             h, self.handle = self.handle, None
             if h and self._wrapped:
-                QueueStream._retired.append((h, self._torch))  # the exit hook destroys h
+                qs = QueueStream.__new__(QueueStream)
+                qs.handle, qs.device = h, self.device
+                qs._torch, qs._wrapped, qs._pooled = self._torch, True, True
+                QueueStream._pool.setdefault(self.device, []).append(qs)
                 h = None
         self._torch = None
         if h:
@@ -314,5 +325,14 @@ def _current_device():
     return 0
 
 
+def counts_host(counts_tensor):
+    """A device counts tensor (int64, torch) read back to a numpy array, checked
+    (check_counts): the safe way to consume rc_chunk_device's counts."""
+    c = counts_tensor.cpu().numpy()
+    check_counts(c)
+    return c
+
+
 __all__ = ['GpuChunker', 'QueueStream', 'normalize_params', 'keys_needed', 'fill_splitmix', 'tables_key',
-           'MIN_LENGTH', 'MAX_LENGTH', '_lib']
+           'check_counts', 'counts_host', 'ChunkerError', 'ChunkerFault', 'MIN_LENGTH', 'MAX_LENGTH',
+           '_lib']

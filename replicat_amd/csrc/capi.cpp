@@ -21,6 +21,8 @@
 
 using namespace rc;
 
+static_assert(kCountFault == RC_COUNT_FAULT && kCtrFaultsWord * 4 < 256, "counter buffer layout");
+
 constexpr uint64_t kDigestSlot = RC_DIGEST_SLOT;
 
 namespace {
@@ -225,8 +227,10 @@ struct rc_chunker {
         DevBuf d_records;   // one TileRecord per tile
         DevBuf d_scratch;   // speculative chain lists of multi-segment streams
         DevBuf d_seg_counts;  // one count (+ termination bit) per chain segment
-        DevBuf d_ctr;         // the tile kernel's grab counter (zeroed once, then by the edge kernel)
+        DevBuf d_ctr;         // the tile kernel's counter buffer (gclmul.h kCtrErrWord): grab
+                              // counter, fail-safe flag, fault stamp and count
         bool ctr_dirty = false;  // a launch failed between the tile and the edge kernel: re-zero it
+        uint64_t epoch = 0;      // this workspace's last launch (the edge kernel's fault stamp)
         std::vector<uint64_t> xtiles;  // host list of the tiles the fast path does not take
         hipEvent_t done = nullptr;  // the call that last used this workspace has finished
         bool pending = false;
@@ -467,28 +471,44 @@ size_t records_bytes(const Plan &plan) {
 // launch grabs its units from this counter -- a tile kernel that started before the memset had
 // landed read whatever the fresh allocation held (a GPU test saw a fresh chunker's first call
 // come back with garbage counts once).
+// A dirty buffer is re-zeroed up to the fault stamp: the fault count (kCtrFaultsWord) is kept
+// for rc_chunker_check.
 int ensure_ctr(Workspace &ws, hipStream_t st) {
+    size_t zero = kCtrFaultsWord * 4;
     if (!ws.d_ctr.p) {
         if (int rc = ws.d_ctr.ensure(256)) return rc;
         ws.ctr_dirty = true;
+        zero = 256;
     }
     if (ws.ctr_dirty) {
-        HIP_TRY(hipMemsetAsync(ws.d_ctr.p, 0, 256, st));
+        HIP_TRY(hipMemsetAsync(ws.d_ctr.p, 0, zero, st));
         ws.ctr_dirty = false;
     }
     return 0;
 }
 
-// The tile kernel's fail-safe flag (kernels.hip UnitGrab::next, word 32 of the counter buffer):
-// a wave that waited ~1 s for a grab published through LDS stopped instead of hanging.  Blocking
-// read; the caller has synchronised.
+const char kFaultMsg[] =
+    "tile kernel fail-safe stop: a workgroup grab was never published, so the launch's records "
+    "are incomplete and its cuts are not the reference's";
+
+// Did the workspace's last launch take the tile kernel's fail-safe stop (kernels.hip
+// UnitGrab::next; the edge kernel stamps the launch's epoch)?  Blocking read; the caller has
+// synchronised.
 int grab_fault(Workspace &ws) {
+    if (!ws.d_ctr.p || !ws.epoch) return 0;
+    uint64_t stamp = 0;
+    HIP_TRY(hipMemcpy(&stamp, static_cast<uint32_t *>(ws.d_ctr.p) + kCtrStampWord, 8,
+                      hipMemcpyDeviceToHost));
+    return stamp == ws.epoch ? fail(RC_ERR_DEVICE_FAULT, "%s", kFaultMsg) : 0;
+}
+
+// The faults the workspace's launches counted since the last call (rc_chunker_check), reset.
+int take_faults(Workspace &ws, uint32_t &n) {
+    n = 0;
     if (!ws.d_ctr.p) return 0;
-    uint32_t flag = 0;
-    HIP_TRY(hipMemcpy(&flag, static_cast<uint32_t *>(ws.d_ctr.p) + 32, 4, hipMemcpyDeviceToHost));
-    if (flag)
-        return fail(RC_ERR_HIP, "tile kernel: a workgroup grab was never published (fail-safe "
-                                "stop; records of that launch are incomplete)");
+    uint32_t *w = static_cast<uint32_t *>(ws.d_ctr.p) + kCtrFaultsWord;
+    HIP_TRY(hipMemcpy(&n, w, 4, hipMemcpyDeviceToHost));
+    if (n) HIP_TRY(hipMemset(w, 0, 4));
     return 0;
 }
 
@@ -545,6 +565,9 @@ int upload_and_launch(rc_chunker *ch, Workspace &ws, const Plan &plan, ChainPara
     }
     HIP_TRY(hipStreamWaitEvent(ts, ch->uploaded[wi], 0));
     if (int rc = ensure_ctr(ws, ts)) return rc;
+    // the call's epoch: its chain kernels compare it with the edge kernel's fault stamp
+    prm.fault = reinterpret_cast<const uint64_t *>(static_cast<uint32_t *>(ws.d_ctr.p) + kCtrStampWord);
+    prm.epoch = ++ws.epoch;
     const StreamDesc d = desc_view(ws.d_desc.p, plan.n);
     std::array<hipEvent_t, 4> ev{};
     if (ch->timing) {
@@ -579,7 +602,8 @@ int upload_and_launch(rc_chunker *ch, Workspace &ws, const Plan &plan, ChainPara
     prm.hot = group_hot_threshold(ch->window);
     if (rc_launch_tiles(ch->d_tables, d, plan.n, plan.n_tiles,
                         static_cast<TileRecord *>(ws.d_records.p), grp, prm.hot, tie_lists(ws, plan),
-                        static_cast<uint32_t *>(ws.d_ctr.p), ts, ch->timing ? ev[1] : nullptr,
+                        static_cast<uint32_t *>(ws.d_ctr.p), prm.epoch, ts,
+                        ch->timing ? ev[1] : nullptr,
                         pipelined ? ch->tile_cus : 0u, xs,
                         // the timing event after the tile kernel doubles as the hand-over event
                         !pipelined ? nullptr : ch->timing ? ev[1] : ch->tiled[wi], ch->sched))
@@ -693,6 +717,8 @@ ChainParams chain_params(const rc_chunker *ch, const Plan &plan, uint64_t max_st
     p.lean = 0;
     p.lane = 0;
     p.hot = 0;
+    p.fault = nullptr;  // set per launch (upload_and_launch)
+    p.epoch = 0;
     return p;
 }
 
@@ -937,6 +963,7 @@ int rc_next_cut(rc_chunker *ch, const uint8_t *buffer, uint64_t size, int final,
     HIP_TRY(hipMemcpyAsync(ch->h_out.p, d_cut, 16, hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     const uint64_t *h = static_cast<const uint64_t *>(ch->h_out.p);
+    if ((int64_t)h[1] == kCountFault) return fail(RC_ERR_DEVICE_FAULT, "%s", kFaultMsg);
     if ((int64_t)h[1] != 1) return fail(RC_ERR_OVERFLOW, "device chain returned %lld cuts", (long long)h[1]);
     *out_cut = h[0];
     return RC_OK;
@@ -1037,10 +1064,15 @@ int rc_chunker_check(rc_chunker *ch) {
     if (!ch) return fail(RC_ERR_ARGUMENT, "null chunker");
     std::lock_guard<std::mutex> lock(ch->mu);
     DeviceGuard g(ch->device);
+    uint32_t faults = 0;
     for (auto &w : ch->ws) {
         if (w.pending) HIP_TRY(hipEventSynchronize(w.done));
-        if (int rc = grab_fault(w)) return rc;
+        uint32_t n = 0;
+        if (int rc = take_faults(w, n)) return rc;
+        faults += n;
     }
+    if (faults)
+        return fail(RC_ERR_DEVICE_FAULT, "%s (%u call(s) since the last check)", kFaultMsg, faults);
     return RC_OK;
 }
 
@@ -1092,10 +1124,12 @@ int chunk_host_impl(rc_chunker *ch, rc_hasher *hasher, uint64_t n, const uint8_t
         HIP_TRY(hipStreamSynchronize(ch->hstream[slot]));
         busy[slot] = false;
         const Batch &b = inflight[slot];
-        for (uint64_t i = 0; i < b.count; ++i)
+        for (uint64_t i = 0; i < b.count; ++i) {
+            if (counts[b.first + i] == kCountFault) return fail(RC_ERR_DEVICE_FAULT, "%s", kFaultMsg);
             if (counts[b.first + i] < 0)
                 return fail(RC_ERR_OVERFLOW, "stream %llu overflowed its cut capacity",
                             (unsigned long long)(b.first + i));
+        }
         return 0;
     };
 
@@ -1199,8 +1233,8 @@ int rc_tile_records(rc_chunker *ch, uint64_t n, const uint8_t *const *d_streams,
     if (rc_launch_tiles(ch->d_tables, desc_view(ws.d_desc.p, n), n, plan.n_tiles,
                         static_cast<TileRecord *>(ws.d_records.p), d_grp,
                         group_hot_threshold(ch->window), tie_lists(ws, plan),
-                        static_cast<uint32_t *>(ws.d_ctr.p), nullptr, nullptr, 0u, nullptr, nullptr,
-                        ch->sched))
+                        static_cast<uint32_t *>(ws.d_ctr.p), ++ws.epoch, nullptr, nullptr, 0u,
+                        nullptr, nullptr, ch->sched))
         return abandon_launch(ws, nullptr, nullptr, fail(RC_ERR_HIP, "%s", rc_launch_error()));
     HIP_TRY(hipDeviceSynchronize());
     if (int rc = grab_fault(ws)) return rc;

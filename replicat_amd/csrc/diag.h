@@ -27,6 +27,17 @@
 #define RC_DIAG_SLICE_FENCE true
 #endif
 
+// ---- a forced fail-safe stop of the tile kernel (-DRC_DIAG_GRAB_FAULT, diag/lib_GRABFAULT.so):
+// wave 1 of workgroup 0 stops at its first workgroup grab -- the unit it took is never run --
+// and sets the fail-safe flag, as a wave whose slot was never published would (UnitGrab::next).
+// Every launch with tiles faults; tests/test_gpu_fault.py checks that every product surface
+// reports it instead of returning cuts.
+#ifdef RC_DIAG_GRAB_FAULT
+#define RC_DIAG_FORCE_GRAB_STOP() (blockIdx.x == 0 && (threadIdx.x >> 6) == 1)
+#else
+#define RC_DIAG_FORCE_GRAB_STOP() false
+#endif
+
 // ---- per-wave stamps of the tile kernel: s_memrealtime (100 MHz) when a wave's first tile
 // starts and when its last record is stored, and its tile count
 #ifdef RC_DIAG_TILE_STAMPS

@@ -108,7 +108,23 @@ struct ChainParams {
     uint32_t lean;        // small windows and every stream < 16 GiB: 32-bit chain steps
     uint32_t lane;        // lane-per-stream chain allowed (rc_lane_chain_kernel; 2 = forced)
     uint32_t hot;         // the group records' hot threshold (group_hot_threshold)
+    // the call's fault stamp (the workspace counter buffer's kCtrStampWord, written by the
+    // edge kernel) and this call's epoch: equal = the tile kernel took its fail-safe stop, the
+    // records are incomplete, and the chain kernels write RC_COUNT_FAULT instead of cuts
+    const uint64_t *fault;
+    uint64_t epoch;
 };
+
+// The tile kernel's counter buffer (256 bytes per workspace, capi.cpp ensure_ctr), in u32 words:
+//   0            the dynamic units' grab counter (the edge kernel re-zeroes it for the next launch)
+//   kCtrErrWord  the fail-safe flag: set by a tile-kernel wave that stopped (UnitGrab::next);
+//                the edge kernel moves it into the stamp below and clears it
+//   kCtrStampWord (u64) the epoch of the last call whose tile kernel set the flag
+//   kCtrFaultsWord how many calls set it since the last rc_chunker_check
+constexpr uint32_t kCtrErrWord = 32, kCtrStampWord = 34, kCtrFaultsWord = 36;
+// Count written for every stream of a faulted call (include/replicat_chunker.h RC_COUNT_FAULT;
+// -1 is a capacity overflow, -2 the chain kernels' internal kNeedJoin)
+constexpr int64_t kCountFault = -3;
 
 // The tile kernel's work schedule (kernels.hip tile_units; knobs.h RC_TILE_STATIC / CHUNK /
 // DYN_MIN): the share of the tiles handed out statically (per mille), the dynamic unit size and
@@ -138,16 +154,18 @@ extern "C" {
 // the chain's bounds for small windows.  mid_event (a hipEvent_t, may be NULL):
 // recorded between the tile and the edge kernel.
 // d_xlist: rc_tie_list_words(n_tiles) u32 of scratch: the tile kernel's tie lists (n_tiles
-// slots) and one count per work unit.  d_ctr: the dynamic units' grab counter, 0 at the call;
-// the edge kernel zeros it again for the next launch.
+// slots) and one count per work unit.  d_ctr: the counter buffer (kCtrErrWord above): the grab
+// counter is 0 at the call and the edge kernel zeros it again for the next launch; `epoch`
+// (this call's, never 0) is what the edge kernel stamps when the tile kernel took its fail-safe
+// stop, and the edge kernel then recomputes nothing (the tie lists may be stale).
 // cus: the CUs the tile kernel's stream may use (its persistent grid; 0 = every CU of the
 // device).  edge_stream (may be NULL = stream): where the edge kernel runs; when it differs,
 // `tiled` (a hipEvent_t) is recorded after the tile kernel and edge_stream waits for it.
 // sched: the chunker's schedule knobs.
 int rc_launch_tiles(const rc::KeyTables *d_tables, rc::StreamDesc desc, uint64_t n_streams,
                     uint64_t n_tiles, rc::TileRecord *d_records, rc::GroupRecord *d_grp,
-                    uint32_t hot, uint32_t *d_xlist, uint32_t *d_ctr, void *stream,
-                    void *mid_event, uint32_t cus, void *edge_stream, void *tiled,
+                    uint32_t hot, uint32_t *d_xlist, uint32_t *d_ctr, uint64_t epoch,
+                    void *stream, void *mid_event, uint32_t cus, void *edge_stream, void *tiled,
                     rc::TileSched sched);
 uint64_t rc_tie_list_words(uint64_t n_tiles);
 // (exported for tests: include/replicat_chunker.h rc_tile_schedule)

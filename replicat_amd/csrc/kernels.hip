@@ -565,6 +565,7 @@ struct TileUnits {  // tile indices fit 32 bits (the tie lists store them as u32
 // RC_TILE_GROUP (sched.group, rounded down to a power of two): the units come in groups of that
 // many, one global grab per group, dealt to the workgroup's waves through LDS (UnitGrab).
 constexpr uint64_t kDynChunkMin = 2;    // units of at least 2 tiles
+constexpr uint32_t kGrabMinShift = 4;   // groups of at least 16 units (UnitGrab's LDS ring)
 __host__ inline TileUnits tile_units(uint64_t n_tiles, uint64_t nw, TileSched sched) {
     TileUnits U;
     U.n_tiles = (uint32_t)n_tiles;
@@ -589,8 +590,10 @@ __host__ inline TileUnits tile_units(uint64_t n_tiles, uint64_t nw, TileSched sc
     U.dyn0 = (uint32_t)(nw * U.s0);
     U.n_units = (uint32_t)(nw + (n_tiles - U.dyn0 + chunk - 1) / chunk);
     if (sched.group) {
+        // at least 2^kGrabMinShift units per group: the LDS ring's margin (UnitGrab)
         uint32_t sh = 0;
         while ((2u << sh) <= sched.group && sh < 8) ++sh;
+        if (sh < kGrabMinShift) sh = kGrabMinShift;
         U.gshift = sh;
         U.n_groups = (uint32_t)(((uint64_t)(U.n_units - U.nw) + (1u << sh) - 1) >> sh);
     }
@@ -620,6 +623,11 @@ __host__ inline TileUnits tile_units(uint64_t n_tiles, uint64_t nw, TileSched sc
 // A wave stops at the first unit past the end; every later ordinal of its workgroup is past the
 // end too (the grabs increase), and every earlier one was taken by a wave that runs it: each
 // unit is run exactly once.  Global grabs drop by 2^gshift, so units can be short.
+// The ring holds kGrabSlots groups: slot k + kGrabSlots overwrites slot k once the other waves
+// have taken ~15 * 2^gshift more ordinals (tile_units keeps gshift >= 4: 240 units, ~0.45 ms of
+// 15 waves' work, between a wave's ordinal and its next LDS read).  A wave that finds a later
+// tag in its slot lagged that far: its group index is lost, so it takes the fail-safe stop at
+// once instead of waiting for a tag that never comes back.
 constexpr uint32_t kGrabSlots = 16;
 constexpr uint32_t kGrabSpinLimit = 1u << 24;  // ~1-2 s of s_sleep waits
 __shared__ uint32_t s_grab_ord;
@@ -627,9 +635,8 @@ __shared__ uint32_t s_grab_cfg[2];  // gshift, n_groups: read from LDS at a swit
                                     // loop holds no SGPRs for them (it is at its SGPR limit)
 __shared__ uint64_t s_grab_slot[kGrabSlots];
 
-// the tile kernel's counter buffer (256 bytes, zeroed once per workspace): word 0 the grab
-// counter (re-zeroed by the edge kernel), this word the sticky fail-safe flag of UnitGrab::next
-constexpr uint32_t kGrabErrWord = 32;
+// the fail-safe flag's word in the tile kernel's counter buffer (gclmul.h kCtrErrWord)
+constexpr uint32_t kGrabErrWord = kCtrErrWord;
 
 template <bool kGroup>
 struct UnitGrab {
@@ -653,9 +660,11 @@ struct UnitGrab {
         for (uint32_t i = 1; i < kGrabSlots; ++i) s_grab_slot[i] = ~0ull;
     }
     // The wave's next dynamic unit; U.n_units or more: none left.
-    // err (may be NULL): set to 1 if a slot stayed unpublished for ~kGrabSpinLimit waits (a
-    // protocol failure: the wave then stops as if the units had run out, so the launch ends
-    // with wrong records instead of hanging the GPU).
+    // err (may be NULL): set to 1 if a slot stayed unpublished for ~kGrabSpinLimit waits or was
+    // overwritten before this wave read it (a protocol failure: the wave then stops as if the
+    // units had run out, so the launch ends with incomplete records instead of hanging the GPU;
+    // the edge kernel turns the flag into the call's fault stamp and every stream's count into
+    // RC_COUNT_FAULT, so no caller receives those cuts as results).
     __device__ uint32_t next(const TileUnits &U, uint32_t *ctr, uint32_t *err) {
         if (U.n_units <= U.nw) return U.n_units;
         if constexpr (!kGroup) {
@@ -674,11 +683,14 @@ struct UnitGrab {
         for (uint32_t spins = 0;; ++spins) {
             const uint64_t e = __hip_atomic_load(&s_grab_slot[k % kGrabSlots], __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_WORKGROUP);
-            if ((uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(e >> 32)) == k) {
+            const uint32_t tag = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(e >> 32));
+            if (tag == k) {
                 g = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)e);
                 break;
             }
-            if (spins == kGrabSpinLimit) {  // fail-safe (never seen): stop, flag it, no hang
+            // fail-safe (never seen): a later group in the slot (this wave lagged a whole ring)
+            // or ~1 s without a publisher -- stop, flag it, no hang.  ~0 tags: not yet written
+            if ((tag != ~0u && (int32_t)(tag - k) > 0) || spins == kGrabSpinLimit) {
                 if (err && lane_id() == 0) atomicOr(err, 1u);
                 break;
             }
@@ -692,6 +704,10 @@ struct UnitGrab {
             if (lane_id() == 0)
                 __hip_atomic_store(&s_grab_slot[(k + 1) % kGrabSlots], ((uint64_t)(k + 1) << 32) | nv,
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        if (RC_DIAG_FORCE_GRAB_STOP() && err) {  // diagnostic build: this unit is never run
+            if (lane_id() == 0) atomicOr(err, 1u);
+            return U.n_units;
         }
         return live ? U.nw + (g << gshift) + sub : U.n_units;
     }
@@ -962,11 +978,34 @@ __global__ __launch_bounds__(256) void rc_edge_kernel(const KeyTables *__restric
                                                       GroupRecord *__restrict__ grp,
                                                       const uint32_t *__restrict__ xlist,
                                                       const uint32_t *__restrict__ xcount,
-                                                      uint32_t *__restrict__ ctr) {
+                                                      uint32_t *__restrict__ ctr, uint64_t epoch) {
     __shared__ __attribute__((aligned(16))) uint64_t s_full[2048];
-    // the tile kernel is done with its grab counter: zero it for the workspace's next launch
-    // (round 3: replaces a hipMemsetAsync between consecutive tile kernels)
-    if (blockIdx.x == 0 && threadIdx.x == 0) *ctr = 0u;
+    __shared__ uint32_t s_fault;
+    // The tile kernel is done with its grab counter: zero it for the workspace's next launch
+    // (round 3: replaces a hipMemsetAsync between consecutive tile kernels).  Its fail-safe flag
+    // (UnitGrab::next) becomes this call's fault stamp -- which the chain kernels read -- and
+    // the flag is cleared: workgroup 0 stores the stamp, counts the fault, then clears the flag
+    // with release order, so a workgroup that reads the flag (acquire) either sees it set or
+    // sees the stamp.  A faulted call's tie lists may be stale (units no wave ran never wrote
+    // their counts), so then nothing is recomputed.
+    if (threadIdx.x == 0) {
+        uint32_t *err = ctr + kCtrErrWord;
+        uint64_t *stamp = reinterpret_cast<uint64_t *>(ctr + kCtrStampWord);
+        uint32_t f = __hip_atomic_load(err, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        if (blockIdx.x == 0) {
+            *ctr = 0u;
+            if (f) {
+                __hip_atomic_store(stamp, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                atomicAdd(ctr + kCtrFaultsWord, 1u);
+                __hip_atomic_store(err, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        } else if (!f) {
+            f = __hip_atomic_load(stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+        }
+        s_fault = f;
+    }
+    __syncthreads();
+    if (s_fault) return;
     const uint64_t gw = (uint64_t)blockIdx.x * (blockDim.x >> 6) +
                         __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
@@ -1027,6 +1066,19 @@ __global__ __launch_bounds__(256) void rc_edge_kernel(const KeyTables *__restric
 // segment i's list at the first position both chains share -- from there the two are the
 // same chain.  Chains normally meet within a chunk; if a list runs out first, the join kernel
 // computes the missing steps itself, so the result is exact in every case.
+
+// The call's fault stamp (rc_edge_kernel): its tile kernel took the fail-safe stop, so its
+// records are incomplete.  Read once per wave at the start of every chain kernel (uniform over
+// the grid: written before the launch); the kernels then walk nothing and every stream's count
+// becomes kCountFault (fault_counts), which every host path reports as an error.
+__device__ __forceinline__ bool call_faulted(const ChainParams &prm) {
+    return prm.fault != nullptr && sload(prm.fault) == prm.epoch;
+}
+__device__ __forceinline__ void fault_counts(int64_t *counts, uint64_t n_streams) {
+    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n_streams;
+         s += (uint64_t)gridDim.x * blockDim.x)
+        counts[s] = kCountFault;
+}
 
 struct ChainStream {
     const uint8_t *base;
@@ -1649,6 +1701,10 @@ __global__ __launch_bounds__(kChainWaves * 64) void rc_spec_kernel(const KeyTabl
                                                       uint64_t *__restrict__ scratch,
                                                       uint64_t *__restrict__ seg_counts,
                                                       uint64_t *__restrict__ seg_rcount) {
+    if (call_faulted(prm)) {  // the merge / scan / mark kernels after it return too
+        fault_counts(counts, n_streams);
+        return;
+    }
     stage_chain_tables(tab);
     const uint32_t *pf = s_chain_lds;
     const uint64_t *full = reinterpret_cast<const uint64_t *>(s_chain_lds + 1024);
@@ -1899,6 +1955,10 @@ __global__ __launch_bounds__(256) void rc_lane_chain_kernel(const KeyTables *__r
                                                             const TileRecord *__restrict__ rec,
                                                             uint64_t *__restrict__ cuts,
                                                             int64_t *__restrict__ counts) {
+    if (call_faulted(prm)) {
+        fault_counts(counts, n_streams);
+        return;
+    }
     stage_chain_tables(tab);
     const uint32_t *pf = s_chain_lds;
     const uint64_t *full = reinterpret_cast<const uint64_t *>(s_chain_lds + 1024);
@@ -2195,6 +2255,10 @@ __global__ __launch_bounds__(256) void rc_quad_chain_kernel(const KeyTables *__r
                                                             uint64_t *__restrict__ cuts,
                                                             int64_t *__restrict__ counts) {
     static_assert(F % 4 == 0 && kLaneIters == 4, "a quad lane per record row and per iteration");
+    if (call_faulted(prm)) {
+        fault_counts(counts, n_streams);
+        return;
+    }
     stage_chain_tables(tab);
     const uint32_t *pf = s_chain_lds;
     const uint64_t *full = reinterpret_cast<const uint64_t *>(s_chain_lds + 1024);
@@ -2439,6 +2503,7 @@ __global__ __launch_bounds__(256) void rc_merge_kernel(const KeyTables *__restri
                                                        uint64_t *__restrict__ seg_merge,
                                                        uint64_t *__restrict__ seg_rcount,
                                                        bool repair) {
+    if (call_faulted(prm)) return;  // the spec lists were never written (rc_spec_kernel)
     const uint32_t lane = lane_id();
     const uint64_t q = (uint64_t)blockIdx.x * (blockDim.x >> 6) +
                        __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2548,12 +2613,14 @@ __global__ __launch_bounds__(256) void rc_merge_kernel(const KeyTables *__restri
 }
 
 __global__ __launch_bounds__(256) void rc_scan_kernel(StreamDesc d, uint64_t n_streams,
+                                                      ChainParams prm,
                                                       const uint64_t *__restrict__ seg_counts,
                                                       const uint64_t *__restrict__ seg_merge,
                                                       const uint64_t *__restrict__ seg_rcount,
                                                       uint64_t *__restrict__ seg_off,
                                                       uint64_t *__restrict__ seg_slice,
                                                       int64_t *__restrict__ counts) {
+    if (call_faulted(prm)) return;  // counts hold kCountFault (rc_spec_kernel): copy and join skip
     const uint32_t lane = lane_id();
     const uint64_t s = (uint64_t)blockIdx.x * (blockDim.x >> 6) +
                        __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2652,7 +2719,8 @@ __global__ __launch_bounds__(256) void rc_copy_kernel(StreamDesc d, uint64_t n_s
 
 // RC_JOIN_WALK=1 (tests, diagnostics): every multi-segment stream takes the sequential walk.
 __global__ __launch_bounds__(256) void rc_mark_kernel(StreamDesc d, uint64_t n_streams,
-                                                      int64_t *__restrict__ counts) {
+                                                      ChainParams prm, int64_t *__restrict__ counts) {
+    if (call_faulted(prm)) return;
     const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (s < n_streams && sload(d.seg_base + s + 1) - sload(d.seg_base + s) > 1)
         counts[s] = kNeedJoin;
@@ -2938,9 +3006,9 @@ const char *rc_launch_error(void) { return g_launch_err; }
 
 int rc_launch_tiles(const KeyTables *d_tables, StreamDesc desc, uint64_t n_streams,
                     uint64_t n_tiles, TileRecord *d_records, GroupRecord *d_grp,
-                    uint32_t hot, uint32_t *d_xlist, uint32_t *d_ctr, void *stream,
-                    void *mid_event, uint32_t tile_cus, void *edge_stream, void *tiled,
-                    TileSched sched) {
+                    uint32_t hot, uint32_t *d_xlist, uint32_t *d_ctr, uint64_t epoch,
+                    void *stream, void *mid_event, uint32_t tile_cus, void *edge_stream,
+                    void *tiled, TileSched sched) {
     hipStream_t st = (hipStream_t)stream;
     hipStream_t est = edge_stream ? (hipStream_t)edge_stream : st;
     // the edge kernel's stream follows the tile kernel (also when there are no tiles)
@@ -2998,7 +3066,7 @@ int rc_launch_tiles(const KeyTables *d_tables, StreamDesc desc, uint64_t n_strea
     if (egrid == 0) egrid = 1;
     hipLaunchKernelGGL(rc_edge_kernel, dim3((unsigned)egrid), dim3(256), 0, est, d_tables, desc,
                        n_streams, U, d_records, d_grp, (const uint32_t *)d_xlist,
-                       (const uint32_t *)d_xcount, d_ctr);
+                       (const uint32_t *)d_xcount, d_ctr, epoch);
     return launch_status("rc_edge_kernel");
 }
 
@@ -3084,7 +3152,7 @@ int rc_launch_chain(const KeyTables *d_tables, StreamDesc desc, uint64_t n_strea
                                (const uint64_t *)d_seg_counts, seg_merge, seg_rcount, repair);
         if (launch_status("rc_merge_kernel")) return 1;
         hipLaunchKernelGGL(rc_scan_kernel, dim3((unsigned)jgrid), dim3(kChainWaves * kWaveSize), 0,
-                           st, desc, n_streams, (const uint64_t *)d_seg_counts,
+                           st, desc, n_streams, prm, (const uint64_t *)d_seg_counts,
                            (const uint64_t *)seg_merge, (const uint64_t *)seg_rcount, seg_off,
                            seg_slice, d_counts);
         if (launch_status("rc_scan_kernel")) return 1;
@@ -3095,7 +3163,7 @@ int rc_launch_chain(const KeyTables *d_tables, StreamDesc desc, uint64_t n_strea
         if (launch_status("rc_copy_kernel")) return 1;
     } else {
         hipLaunchKernelGGL(rc_mark_kernel, dim3((unsigned)jgrid), dim3(kChainWaves * kWaveSize), 0,
-                           st, desc, n_streams, d_counts);
+                           st, desc, n_streams, prm, d_counts);
         if (launch_status("rc_mark_kernel")) return 1;
     }
     if (small)

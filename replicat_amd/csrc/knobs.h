@@ -95,7 +95,8 @@ inline constexpr KnobSpec kKnobTable[kKnobCount] = {
      "may start on CUs the previous one has left"},
     {"RC_TILE_GROUP", 64, 0, 256, nullptr,
      "dynamic units per workgroup grab of the tile kernel (a power of two: the workgroup's "
-     "waves take that many units from one global grab through LDS); 0: one grab per unit"},
+     "waves take that many units from one global grab through LDS; below 16 runs as 16, the "
+     "LDS ring's margin); 0: one grab per unit"},
     {"RC_TILE_MASK", 0, 0, 2, "masked|full|plain",
      "tile stream of pipelined calls: masked (the CUs the chain stream does not reserve), full "
      "(its own queue with every CU in its mask) or plain (a non-blocking stream on the shared "

@@ -67,7 +67,7 @@ from typing import Dict, List, Optional, Sequence
 import numpy as np
 
 from .chunker import (MAX_LENGTH, MIN_LENGTH, GpuChunker, QueueStream, _current_device,
-                      normalize_params)
+                      check_counts, normalize_params)
 from .hashing import SLOT, GpuBlake2b, state_init
 from .snapshot import PIECE, PieceReader, file_parts, sort_files
 
@@ -559,8 +559,7 @@ class DeviceSnapshotProducer:
                 if prev is not None:
                     prev.ev_cut.synchronize()
                     cnt, cut_end = int(prev.h_meta[0]), int(prev.h_meta[1])
-                    if cnt < 0:
-                        raise RuntimeError('cut capacity overflow')
+                    check_counts([cnt])  # overflow, or the tile kernel's fail-safe stop
                     cut_end = cut_end if cnt else 0
                     T = prev.blen - cut_end
                     if T > self.head:
@@ -702,8 +701,7 @@ class _Run:
         t0 = clock()
         s.ev_done.synchronize()
         count = int(s.h_meta[0])
-        if count < 0:
-            raise RuntimeError('cut capacity overflow')
+        check_counts([count])
         # every device read on the slot's own stream: the legacy NULL stream would wait for
         # every blocking (own-queue) slot stream, i.e. for the later batches' digests too
         with torch.cuda.stream(s.stream):
@@ -852,6 +850,12 @@ class ChunkStream:
                               chunks_table=self._run.table)
 
     def close(self):
+        if threading.current_thread() is self._thread:
+            # finalised on the producer thread itself (a cyclic GC pass may run there): it cannot
+            # wait for itself -- ask it to stop and release what is queued; it ends on its own
+            self._abort.set()
+            self._drain_queued()
+            return
         if self._thread.is_alive():
             self._abort.set()
             while self._thread.is_alive():  # drain (drops unconsumed records, releasing them)
@@ -864,13 +868,16 @@ class ChunkStream:
         # what the producer queued before it stopped: release those records now (round 5: with
         # 3 slots a whole batch of them could sit here, holding its slot's lease, until this
         # stream was garbage-collected -- and the next run on the producer waited for it)
+        self._drain_queued()
+        self._done = True
+
+    def _drain_queued(self):
         import queue
         while True:
             try:
                 self._drop(self._q.get_nowait())
             except queue.Empty:
                 break
-        self._done = True
 
     @staticmethod
     def _drop(item):

@@ -41,6 +41,9 @@ class OracleChunker:
     def wait(self, stream=0):
         pass
 
+    def check(self):  # the oracle has no tile kernel, so no fail-safe stop
+        pass
+
     def pipelined_calls(self):
         return self.pipelined_calls_n
 

@@ -46,8 +46,18 @@ with torch.cuda.stream(qs.torch):
     x = torch.arange(1 << 20, dtype=torch.int64, device='cuda')
     y = (x * 7).sum()
 x.record_stream(qs.torch)  # torch records an event on qs when x is freed
-qs.close()                 # retired, not destroyed: torch still knows the stream
-assert qs.handle is None and len(QueueStream._retired) == 1
+h = qs.handle
+qs.close()                 # back to the pool, not destroyed: torch still knows the stream
+assert qs.handle is None and [p.handle for p in QueueStream._pool[0]] == [h]
+again = QueueStream.acquire(0)  # the same stream, a fresh wrapper (ADVICE r5: no leak)
+assert again is not qs and again.handle == h and again.torch is not None
+again.close()
+for _ in range(5):         # acquire / use under torch / close cycles keep ONE stream
+    q2 = QueueStream.acquire(0)
+    with torch.cuda.stream(q2.torch):
+        (torch.ones(16, device='cuda') * 2).sum()
+    q2.close()
+assert [p.handle for p in QueueStream._pool[0]] == [h]
 del x                      # the freed block's event is recorded on the retired stream
 z = torch.ones(1 << 22, device='cuda')
 for _ in range(8):

@@ -25,10 +25,11 @@ from replicat_amd import synth  # noqa: E402
 from replicat_amd.chunker import GpuChunker  # noqa: E402
 
 # (static per mille, unit tiles, units per workgroup grab): fully static (round 2), the round-3/4
-# per-wave grabs, small per-wave units, and workgroup grabs of 2 to 256 units (the default since
-# round 5 is 0:3:64, which every other GPU test runs)
+# per-wave grabs, small per-wave units, and workgroup grabs of 16 to 256 units (the default since
+# round 5 is 0:3:64, which every other GPU test runs; groups below 16 run as 16 since round 6 --
+# the LDS ring's margin, kernels.hip UnitGrab)
 SCHEDULES = [('1000', '12', '0'), ('100', '12', '0'), ('0', '2', '0'), ('900', '7', '0'),
-             ('0', '2', '2'), ('100', '3', '32'), ('0', '2', '256'), ('500', '5', '16')]
+             ('0', '2', '16'), ('100', '3', '32'), ('0', '2', '256'), ('500', '5', '16')]
 
 
 @pytest.fixture(params=SCHEDULES, ids=['s%s_c%s_g%s' % x for x in SCHEDULES])

@@ -4,7 +4,12 @@ published slot of their group, and the taker of a group's first unit issues the 
 grab (an atomic whose value arrives later, in arrival order), waits for it and publishes it
 before it runs its unit.  Checked: every dynamic unit is run exactly once, no wave waits forever (every schedule
 drains), and each workgroup's global grabs increase.  The model follows UnitGrab.next /
-publish statement by statement; it needs no device."""
+publish statement by statement; it needs no device.
+
+Round 6: groups hold at least 16 units (tile_units clamps gshift to 4), and a wave
+that finds a LATER tag in its slot -- it lagged a whole ring of 16 groups -- takes the fail-safe
+stop at once (its group index is lost) instead of spinning ~1 s.  A parked wave models that lag:
+the schedule still drains, no unit runs twice, and a lost unit is always reported as a fault."""
 import random
 
 import pytest
@@ -13,8 +18,11 @@ SLOTS = 16  # kGrabSlots
 
 
 class Sim:
-    def __init__(self, rnd, n_wg, waves, n_units, gshift):
+    def __init__(self, rnd, n_wg, waves, n_units, gshift, park=0):
         self.rnd = rnd
+        self.park = park      # steps the first wave to take an ordinal stays parked after it
+        self.parked = None
+        self.fault = False
         self.K = 1 << gshift
         self.gshift = gshift
         self.n_units = n_units
@@ -79,13 +87,21 @@ class Sim:
             wg['ord'] += 1
             wv['k'], wv['sub'] = o >> self.gshift, o & (self.K - 1)
             wv['state'] = 'spin'
+            if self.park and self.parked is None and wv['sub'] != 0:
+                self.parked = [wv, self.park]
             return True
         if st == 'spin':
+            if self.parked is not None and self.parked[0] is wv and self.parked[1] > 0:
+                self.parked[1] -= 1  # parked: its time passes (not a deadlock)
+                return True
             wg = self.wgs[wv['wg']]
             tag, g = wg['slot'][wv['k'] % SLOTS]
             if tag != wv['k']:
-                assert tag is None or tag < wv['k'], 'slot overwritten before it was read'
-                return False
+                if tag is None or tag < wv['k']:
+                    return False  # not published yet: wait
+                # a later group in the slot: the fail-safe stop (the flag; no group index)
+                self.fault = True
+                g = 1 << 32
             live = g < self.n_groups
             if wv['sub'] == 0:  # grab slot k + 1 now, wait for it, publish it at once
                 wv['pub_k'] = wv['k'] + 1
@@ -122,6 +138,8 @@ class Sim:
 
     def run(self):
         for _ in range(10_000_000):
+            if self.parked is not None and self.parked[1] > 0 and self.rnd.random() < 0.5:
+                self.parked[1] -= 1  # the parked wave's time passes while others run
             live = [w for w in self.waves if w['state'] != 'done']
             if not live and not self.pending:
                 return
@@ -146,10 +164,29 @@ def test_group_grabs_run_every_unit_once(seed):
     rnd = random.Random(seed)
     n_wg = rnd.choice([1, 2, 3, 7])
     waves = rnd.choice([1, 2, 4, 16])
-    gshift = rnd.choice([0, 1, 2, 4, 5])
-    n_units = rnd.choice([0, 1, 5, 31, 32, 33, 97, 300])
+    gshift = rnd.choice([4, 5, 6])  # tile_units: at least 2^kGrabMinShift units per group
+    n_units = rnd.choice([0, 1, 5, 31, 32, 33, 97, 300, 2000])
     sim = Sim(rnd, n_wg, waves, n_units, gshift)
     sim.run()
+    assert not sim.fault
     assert sorted(sim.ran) == list(range(n_units))
     for wg in sim.wgs:
         assert wg['grabs'] == sorted(wg['grabs']), 'a workgroup\'s grabs must increase'
+
+
+@pytest.mark.parametrize("seed", range(60))
+def test_parked_wave_faults_instead_of_hanging(seed):
+    """One wave parks right after taking its ordinal while 15 others of its workgroup run on:
+    short parks change nothing; a park long enough for the ring to come round (16 groups of
+    16+ units) ends in the fail-safe stop at once -- never a hang, never a unit run twice, and a
+    unit is missing only when the fault was reported."""
+    rnd = random.Random(1000 + seed)
+    gshift = 4
+    park = rnd.choice([5, 50, 20_000, 200_000])
+    sim = Sim(rnd, 1, 16, 3000, gshift, park=park)
+    sim.run()
+    assert len(sim.ran) == len(set(sim.ran)), 'a unit ran twice'
+    if not sim.fault:
+        assert sorted(sim.ran) == list(range(3000))
+    else:
+        assert len(sim.ran) < 3000
