@@ -103,6 +103,8 @@ def parse(argv=None):
 
 
 WARMUP_SHORT = 50  # warm-up steps of sub-millisecond configurations (parse)
+WARM_MS = 100.0       # warm-up runs at least this long (main), whatever --warmup says
+WARM_MAX_STEPS = 2000
 
 
 def _free_port():
@@ -475,9 +477,16 @@ def pmc_traffic(workload, build_id):
         if d.get('build_id') != build_id:
             stale = stale or f'{os.path.relpath(f, ROOT)} is of build {d.get("build_id")}, not {build_id}'
             continue
+        PROFILE.clear()
+        if t.get('steady_avg_ns'):
+            PROFILE.update(steady_ns=t['steady_avg_ns'], median_ns=t.get('median_ns'),
+                           launches=t.get('launches'))
         return (t['hbm_read_bytes_corrected'] + t.get('hbm_write_bytes', 0.0),
                 os.path.relpath(f, ROOT) + f' [{workload}]')
     return None, stale or f'no PMC summary of {workload} under profiles/'
+
+
+PROFILE = {}  # the tile kernel's launch times in the PMC summary pmc_traffic() accepted
 
 
 # ------------------------------------------------------------------- config 5 (dedup)
@@ -769,6 +778,22 @@ def roofline(bytes_per_step, read, tile_avg, edge_avg, chain_avg, traffic, traff
     if not ok:
         r['note'] = ('no key is hashed: every stream is cut by the tail rule alone '
                      '(adapters.cpp:48-55); no roofline') if read == 0 else 'not a measurement'
+    # round 6: the same roofline from the committed rocprofv3 trace of this
+    # build and workload (steady state: its first, cold launch dropped), beside the HIP-event one
+    if ok and traffic_src and PROFILE.get('steady_ns'):
+        pf = bytes_per_step / PROFILE['steady_ns'] / HBM_PEAK_GBS
+        r.update({'profile_kernel_ms': round(PROFILE['steady_ns'] * 1e-6, 3),
+                  'profile_frac': round(pf, 4),
+                  'profile_frac_median': round(bytes_per_step / PROFILE['median_ns'] / HBM_PEAK_GBS, 4)
+                  if PROFILE.get('median_ns') else None,
+                  'profile_source': traffic_src.split(' [')[0] + ' (kernel trace, '
+                  f'{PROFILE.get("launches")} launches, first dropped)',
+                  'profile_vs_line': round(pf / r['frac'], 4)})
+        if abs(pf / r['frac'] - 1) > 0.03:
+            r['profile_note'] = ('the profiled process ran on another allocation (or box): '
+                                 'HBM placement moves the tile kernel by up to ~5 % between '
+                                 'allocations (DESIGN.md §4, placement), the profiler also '
+                                 'serialises the pipelined kernels')
     return r
 
 
@@ -871,8 +896,22 @@ def main(argv=None, backend=Backend):
             ch.chunk_device(ptrs_a, lens_a, last_a, cuts.data_ptr(), counts.data_ptr(), hs,
                             pipelined=pipe, end=end)
 
-    for i in range(args.warmup):
-        step(end=i == args.warmup - 1)
+    # warm-up: the requested steps, then more until the warm-up has kept the device busy for
+    # WARM_MS (round 6): the clock ramps over the first ~30-40 ms of work,
+    # which 2 sub-millisecond steps do not cover (profiles/r05/warmup/: the harness 0.857 ms per
+    # tile kernel after 2 steps, 0.792 after 50); every rank runs the same number of steps (the
+    # split line's steps exchange cuts), decided on the slowest rank's time
+    warm_steps, warm_s, tw = 0, 0.0, time.perf_counter()
+    batch = args.warmup
+    while batch > 0:
+        for i in range(batch):
+            step(end=i == batch - 1)
+        warm_steps += batch
+        ch.wait(hs)
+        be.synchronize()
+        warm_s = ranks.max([time.perf_counter() - tw])[0]
+        batch = 0 if warm_s * 1e3 >= WARM_MS or warm_steps >= WARM_MAX_STEPS else \
+            min(max(8, warm_steps), WARM_MAX_STEPS - warm_steps)
     ch.wait(hs)
     be.synchronize()
     ranks.barrier()
@@ -989,6 +1028,8 @@ def main(argv=None, backend=Backend):
             'n_gpus': world,
             'steps': args.steps,
             'warmup': args.warmup,
+            'warmup_run': {'steps': warm_steps, 'ms': round(warm_s * 1e3, 1),
+                           'rule': f'at least --warmup steps and {WARM_MS} ms of them'},
             'ms_per_step': round(ms_per_step, 3),
             'pipeline': {'on': pipelined, 'reserve_cus': reserve, 'pipelined_steps': piped,
                          'unpipelined_ms_per_step': None if seq_ms is None else round(seq_ms, 3),

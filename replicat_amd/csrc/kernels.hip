@@ -283,32 +283,56 @@ __device__ __forceinline__ uint64_t tile_key_end(uint64_t j0, uint64_t L, uint64
     return tile_fast(j0, L) ? j0 + kTileKeys - 1 : min(j0 + kTileKeys - 1, jneed);
 }
 
-constexpr uint32_t kLastLocal = 4 * kTileIters - 1;
 // TileRecord.j of a tile left to the exact path: ~stream index (its key: the candidate lanes;
 // streams are numbered below 2^31 here, checked by the host)
 constexpr uint64_t kTieMark = ~0ull;
+
+// (hi16(a) ^ lo16(b)) << 16 in ONE VALU (SDWA: src0 WORD_1, src1 WORD_0, dst WORD_1, low half
+// zero): the top 16 bits of key j from the prefilter entries of words j-1 (a, its Lmap half) and
+// j (b, its Hmap half).  Round 6: replaces the split of every entry into a masked high half and
+// a shifted low half (two VALU per word) and the per-key index packing (below).
+__device__ __forceinline__ uint32_t key_top16(uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_xor_b32_sdwa %0, %1, %2 dst_sel:WORD_1 dst_unused:UNUSED_PAD src0_sel:WORD_1 "
+        "src1_sel:WORD_0"
+        : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+// an opaque v_max_u32 (as max3_u32: keeps LLVM from re-associating the running maxima)
+__device__ __forceinline__ uint32_t max_u32_op(uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_max_u32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
 
 // Fast path over a tile whose kTileIters loads are in flight in x[].  As iteration `it` consumes
 // x[it] it re-issues x[it] for the wave's NEXT fast tile (if any), so every wave keeps
 // 8 KiB of HBM reads in flight through its compute phase (a register ring: no extra VGPRs,
 // the in-order vmcnt does the bookkeeping).
 //
-// Returns the lane's largest top-16 value and the first and last local index where it occurs.
+// Returns the lane's largest top-16 value `top` and the first and last SLICE (iteration) of the
+// lane holding it, fs and ls (round 6; until round 5 the first and last key, packed per key: two
+// fused XOR-ORs per key).  Per 16-byte slice: 16 table addresses (v_perm), 16 lookups, 4 three-
+// input XOR folds + 4 XORs (the words' entries), the neighbour entry by DPP, 4 SDWA XORs (the
+// keys' top 16 bits), the slice maximum, and the slice index ORed into the two running maxima:
+// 36 VALU instead of 43.  The key inside the slice is found exactly at retire (rc_tile_kernel:
+// the 4 keys of a candidate lane's first slice get exact keys), and a lane whose maximum is in
+// two slices makes the tile a marker, as a key-level tie did.
 // `prev_word` holds the word before the tile (key j0's low half) and is refilled with the next
 // tile's, issued with the ring.
 //
 // G > 1 (chunkers with small windows, see rc_launch_tiles): the tile's keys also fall into G
 // groups of kTileKeys / G consecutive keys (iterations it * G / kTileIters), and the lane's
 // largest top-16 value per group comes back packed two per word in gpk (group g in half g & 1
-// of gpk[g / 2]).  The per-lane maximum then accumulates per group and folds into acc_first at
-// each group's end: one extra v_max per group, not per key.
+// of gpk[g / 2]): one more v_max per slice.
 template <int G>
 __device__ __forceinline__ void tile_scan(const TileRef &tr, const TileRef &nx,
                                           u32x4 (&x)[kTileIters], uint32_t &prev_word,
                                           uint32_t lb_a, uint32_t lb_b, uint32_t &top,
-                                          uint32_t &first, uint32_t &last,
+                                          uint32_t &fs, uint32_t &ls,
                                           uint32_t (&gpk)[(G + 1) / 2]) {
     static_assert(G == 1 || (G % 2 == 0 && kTileIters % G == 0), "groups: 1 or an even divisor");
+    static_assert(kTileIters <= 16, "slice indices: 4 bits");
     constexpr int kPer = kTileIters / G;  // iterations per group
     const uint32_t lane = lane_id();
     // no next fast tile (end of the wave's range): harmlessly re-read this tile instead, so
@@ -321,7 +345,7 @@ __device__ __forceinline__ void tile_scan(const TileRef &tr, const TileRef &nx,
     const uint64_t nj0 = nx.fast ? nx.j0 : tr.j0;
     prev_word = ld_u32(nj0 ? nbase - 4 : nbase);
     // key 0 of a stream (local index 0 of lane 0 in tile 0) does not exist: i starts at 4
-    // (adapters.cpp:59).  Its packed values are zeroed, so it never becomes a lane's maximum.
+    // (adapters.cpp:59).  Its top-16 value is zeroed, so it never raises a slice maximum.
     const uint32_t key0_mask = (tr.j0 == 0 && lane == 0) ? 0u : ~0u;
     uint32_t acc_first = 0, acc_last = 0, acc_grp = 0;
 #pragma unroll
@@ -359,33 +383,27 @@ __device__ __forceinline__ void tile_scan(const TileRef &tr, const TileRef &nx,
         const uint32_t rot = __builtin_amdgcn_mov_dpp(e3, 0x13C, 0xf, 0xf, false);
         const uint32_t ep = lane == 0 ? carry : rot;
         carry = rot;
-        const uint32_t b0 = (ep & 0xffff0000u) ^ (e0 << 16);
-        const uint32_t b1 = (e0 & 0xffff0000u) ^ (e1 << 16);
-        const uint32_t b2 = (e1 & 0xffff0000u) ^ (e2 << 16);
-        const uint32_t b3 = (e2 & 0xffff0000u) ^ (e3 << 16);
-        // local key index l = 4*it + k;  "first" packs kLastLocal - l, "last" packs l
-        const uint32_t inv = kLastLocal - 3u - 4u * it, idx = 4u * it;
-        const uint32_t m0 = it == 0 ? key0_mask : ~0u;
-        if constexpr (G == 1) {
-            acc_first = max3_u32(acc_first, (b0 | inv | 3u) & m0, b1 | inv | 2u);
-            acc_first = max3_u32(acc_first, b2 | inv | 1u, b3 | inv);
-        } else {
-            acc_grp = max3_u32(acc_grp, (b0 | inv | 3u) & m0, b1 | inv | 2u);
-            acc_grp = max3_u32(acc_grp, b2 | inv | 1u, b3 | inv);
+        uint32_t b0 = key_top16(ep, e0);
+        if (it == 0) b0 &= key0_mask;
+        const uint32_t b1 = key_top16(e0, e1), b2 = key_top16(e1, e2), b3 = key_top16(e2, e3);
+        // the slice's maximum; its index ORed in low: "first" prefers the earliest slice
+        // (15 - it), "last" the latest (it)
+        const uint32_t sm = max_u32_op(max3_u32(b0, b1, b2), b3);
+        acc_first = max_u32_op(acc_first, sm | (uint32_t)(kTileIters - 1 - it));
+        acc_last = max_u32_op(acc_last, sm | (uint32_t)it);
+        if constexpr (G > 1) {
+            acc_grp = max_u32_op(acc_grp, sm);
             if ((it + 1) % kPer == 0) {  // compile-time after the unroll
                 const int g = it / kPer;
-                acc_first = max(acc_first, acc_grp);
                 if (g % 2 == 0) gpk[g / 2] = acc_grp >> 16;
                 else gpk[g / 2] |= acc_grp & 0xffff0000u;
                 acc_grp = 0;
             }
         }
-        acc_last = max3_u32(acc_last, (b0 | idx) & m0, b1 | idx | 1u);
-        acc_last = max3_u32(acc_last, b2 | idx | 2u, b3 | idx | 3u);
     }
     top = acc_first >> 16;
-    first = kLastLocal - (acc_first & 0xffffu);
-    last = acc_last & 0xffffu;
+    fs = (uint32_t)(kTileIters - 1) - (acc_first & 0xffffu);
+    ls = acc_last & 0xffffu;
 }
 
 // Maximum over the wave, returned in SGPRs: DPP shifts within each 16-lane row, then the
@@ -787,14 +805,43 @@ __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restri
         }
     }
     // Records are produced one tile late: a tile's candidate words are loaded when it ends and
-    // its exact key is evaluated (and its record stored) at the end of the next tile, when the
-    // load has long landed.  Every tile issues the same vector-memory sequence (ring loads,
+    // its exact keys are evaluated (and its record stored) at the end of the next tile, when the
+    // loads have long landed.  Every tile issues the same vector-memory sequence (ring loads,
     // neighbour word, candidate words, one record store) so the compiler's in-order vmcnt
     // waits stay exact; the first store goes to the spare record at n_tiles.
-    uint64_t pend_t = n_tiles, pend_j0 = 0;  // SGPRs: the pending tile and its first key
-    uint64_t pend_mask = 0;                   // candidate lanes
-    uint32_t pend_st = 0;                     // bit 31: a tie (marker record), low bits: stream
-    uint32_t pend_lo = 0, pend_hi = 0, pend_jl = 0;  // per lane: candidate words and index
+    uint64_t pend_t = n_tiles;  // SGPRs: the pending tile,
+    uint64_t pend_jm = 0;       // its first key | its top-16 maximum M << 48 (j0 < 2^44),
+    uint64_t pend_mask = 0;     // a marker's candidate lanes, else the lanes holding a key
+    uint32_t pend_st = 0;       // bit 31: a marker record, low bits: the stream
+    uint32_t pend_lo = 0, pend_hi = 0, pend_jl = 0;  // per lane: its key's words and index
+
+    // retire the pending tile: the first maximal exact key over the keys the lanes hold (those
+    // whose top 16 bits are M), or the marker the edge kernel resolves
+    auto retire = [&]() {
+        const uint64_t k = full_key(tl, th, pend_lo, pend_hi);
+        const bool ptie = pend_st >> 31;
+        const uint64_t pj0 = pend_jm & ((1ull << 48) - 1);
+        const uint32_t pm = (uint32_t)(pend_jm >> 48);
+        const uint64_t hold = ptie ? 0 : pend_mask;
+        // a marker carries what the edge kernel needs: candidate lanes, ~stream
+        uint64_t bk = ptie ? pend_mask : 0, bj = kTieMark ^ (pend_st & 0x7fffffffu);
+        const bool win = ((hold >> lane) & 1) && (uint32_t)(k >> 48) == pm &&
+                         pj0 + pend_jl != 0;  // key 0 of a stream does not exist
+        const uint64_t wm = __ballot(win);
+        for (uint64_t m = wm; m; m &= m - 1) {  // usually one lane
+            const int l = __builtin_ctzll(m);
+            const uint64_t kl = lane_u64(k, l);
+            const uint64_t jl = pj0 + (uint32_t)__builtin_amdgcn_readlane(pend_jl, l);
+            if (m == wm || kl > bk || (kl == bk && jl < bj)) {
+                bk = kl;
+                bj = jl;
+            }
+        }
+        if (lane == 0) {
+            rec[pend_t].key = bk;
+            rec[pend_t].j = bj;
+        }
+    };
 
     for (;;) {
         // the next fast tile: in this unit, else in the next units (grabbed ones)
@@ -819,55 +866,47 @@ __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restri
             tn = nub;
             if (tn < nue) cursor.init(d, n_streams, tn);
         }
-        uint32_t top, first, last;
+        uint32_t top, fs, ls;
         uint32_t gpk[(G + 1) / 2];
-        tile_scan<G>(cur, nx, x, prev_word, lb_a, lb_b, top, first, last, gpk);
+        tile_scan<G>(cur, nx, x, prev_word, lb_a, lb_b, top, fs, ls, gpk);
         if constexpr (G > 1) {  // this tile's group bounds, stored now (no exact key needed)
             const GroupRecord g = tile_groups<G>(gpk, hot);
             if (lane == 0) grp[t] = g;
         }
 
-        // retire the pending tile: (first maximal exact key, index) over its candidate lanes
-        {
-            const uint64_t k = full_key(tl, th, pend_lo, pend_hi);
-            // a marker carries what the edge kernel needs: candidate lanes, ~stream
-            const bool ptie = pend_st >> 31;
-            const uint64_t pm = ptie ? 0 : pend_mask;
-            uint64_t bk = ptie ? pend_mask : 0, bj = kTieMark ^ (pend_st & 0x7fffffffu);
-            for (uint64_t m = pm; m; m &= m - 1) {  // usually one lane
-                const int l = __builtin_ctzll(m);
-                const uint64_t kl = lane_u64(k, l);
-                const uint64_t jl = pend_j0 + (uint32_t)__builtin_amdgcn_readlane(pend_jl, l);
-                if (m == pm || kl > bk || (kl == bk && jl < bj)) {
-                    bk = kl;
-                    bj = jl;
-                }
-            }
-            if (lane == 0) {
-                rec[pend_t].key = bk;
-                rec[pend_t].j = bj;
+        retire();
+
+        // this tile: its largest top-16 value M; the lanes holding it are the candidates, and
+        // every key that can reach M lies in a candidate lane's first slice holding M -- unless
+        // a candidate holds M in two slices, or there are more than 16 candidates: then the
+        // tile becomes a marker record and the edge kernel recomputes it from the candidate
+        // lanes.  Otherwise lane 4q + k takes key k of the q-th candidate's slice; its exact key
+        // is evaluated one tile later.
+        const uint32_t M = wave_max_u32(top);
+        const bool cand = top == M;
+        const uint64_t cmask = __ballot(cand);
+        const uint32_t nc = (uint32_t)__builtin_popcountll(cmask);
+        const bool tie = __ballot(cand && fs != ls) != 0 || nc > 16;
+        const uint32_t c0 = (uint32_t)__builtin_ctzll(cmask);
+        const uint32_t f0 = (uint32_t)__builtin_amdgcn_readlane(fs, c0);
+        uint32_t jl = f0 * 256 + c0 * 4 + (lane & 3);  // lanes past the last candidate: a copy
+        if (!tie) {
+            uint64_t m = cmask & (cmask - 1);
+            for (uint32_t q = 1; m; m &= m - 1, ++q) {  // the other candidates (rare)
+                const uint32_t c = (uint32_t)__builtin_ctzll(m);
+                const uint32_t f = (uint32_t)__builtin_amdgcn_readlane(fs, c);
+                if ((lane >> 2) == q) jl = f * 256 + c * 4 + (lane & 3);
             }
         }
-
-        // this tile: largest top-16 value, then the lowest tile-local index holding it; the
-        // lanes holding that value are the candidates.  A candidate lane whose maximum occurs
-        // twice cannot name its first maximal key: the tile becomes a marker record and the
-        // edge kernel recomputes it exactly.
-        const uint32_t jl = (first >> 2) * 256 + lane * 4 + (first & 3);
-        const uint32_t p = wave_max_u32((top << 16) | (0xffffu - jl));
-        const bool cand = top == (p >> 16);
-        const uint64_t cmask = __ballot(cand);
-        const bool tie = __any(cand && first != last);
-        const uint32_t win = 0xffffu - (p & 0xffffu);
         if (lane == 0) xlist[ub + n_ties] = (uint32_t)t;  // kept only if it is a tie
         n_ties += tie ? 1u : 0u;
         pend_t = t;
-        pend_j0 = cur.j0;
-        pend_mask = cmask;
+        pend_jm = cur.j0 | ((uint64_t)M << 48);
+        pend_mask = tie ? cmask : (nc >= 16 ? ~0ull : (1ull << (4 * nc)) - 1);
         pend_st = (tie ? 0x80000000u : 0u) | (uint32_t)cur.s;
-        pend_jl = cand ? jl : win;  // non-candidates load the winner's (same) line
+        pend_jl = jl;
         const uint8_t *q = cur.base + 4 * (cur.j0 + pend_jl);
-        pend_lo = ld_u32(q - (cur.j0 + pend_jl ? 4 : 0));  // never key 0; no read before the stream
+        pend_lo = ld_u32(q - (cur.j0 + pend_jl ? 4 : 0));  // no read before the stream
         pend_hi = ld_u32(q);
         RC_TILE_STAMP_TILE();
         if (nu != u) {  // cur was its unit's last fast tile: close the unit's tie list
@@ -881,26 +920,10 @@ __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restri
         t = tn;
         cur = nx;
     }
-    {
-        const uint64_t k = full_key(tl, th, pend_lo, pend_hi);
-        const bool ptie = pend_st >> 31;
-        const uint64_t pm = ptie ? 0 : pend_mask;
-        uint64_t bk = ptie ? pend_mask : 0, bj = kTieMark ^ (pend_st & 0x7fffffffu);
-        for (uint64_t m = pm; m; m &= m - 1) {
-            const int l = __builtin_ctzll(m);
-            const uint64_t kl = lane_u64(k, l);
-            const uint64_t jl = pend_j0 + (uint32_t)__builtin_amdgcn_readlane(pend_jl, l);
-            if (m == pm || kl > bk || (kl == bk && jl < bj)) {
-                bk = kl;
-                bj = jl;
-            }
-        }
-        if (lane == 0) {
-            rec[pend_t].key = bk;
-            rec[pend_t].j = bj;
-            xcount[u] = n_ties;
-            RC_TILE_STAMP_END(gw);
-        }
+    retire();
+    if (lane == 0) {
+        xcount[u] = n_ties;
+        RC_TILE_STAMP_END(gw);
     }
 }
 

@@ -17,7 +17,7 @@ for w in config2 harness config3iii config3ii config5 config2_seeded config4; do
   d=gpurun_out/pmc/$w
   mkdir -p $d
   A="$COMMON ${ARGS[$w]}"
-  timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $d/trace -o run -- python3 bench.py $A > $d/trace.log 2>&1 || { echo "$w trace failed"; tail -5 $d/trace.log; exit 5; }
+  timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $d/trace -o run -- python3 bench.py $A ${TRACE_STEPS:---steps 20} > $d/trace.log 2>&1 || { echo "$w trace failed"; tail -5 $d/trace.log; exit 5; }
   timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "rc_tile|rc_read_probe" --output-format csv -d $d/fetch -o run -- python3 bench.py $A --calibrate > $d/fetch.log 2>&1 || { echo "$w fetch failed"; tail -5 $d/fetch.log; exit 6; }
   timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "rc_tile" --output-format csv -d $d/write -o run -- python3 bench.py $A > $d/write.log 2>&1 || { echo "$w write failed"; tail -5 $d/write.log; exit 7; }
   if [ $w = harness ] || [ $w = config2 ]; then
