@@ -51,9 +51,9 @@ def lib():
         L.oc_tile_records.restype = None
         L.oc_tile_records.argtypes = [_u64, _u64, _p, _u64, _u64, _u64, _u64, _p, _p]
         L.oc_tile_groups.restype = None
-        L.oc_tile_groups.argtypes = [_u64, _u64, _p, _u64, _u64, _u64, _u64, _p]
+        L.oc_tile_groups.argtypes = [_u64, _u64, _p, _u64, _u64, _u64, _u64, _u64, _p]
         L.oc_tile_groups_hot.restype = None
-        L.oc_tile_groups_hot.argtypes = [_u64, _u64, _p, _u64, _u64, _u64, _u64, _u64, _p]
+        L.oc_tile_groups_hot.argtypes = [_u64, _u64, _p, _u64, _u64, _u64, _u64, _u64, _u64, _p]
         L.oc_chunk_streams_mt.restype = ctypes.c_int
         L.oc_chunk_streams_mt.argtypes = [_u64, _u64, _u64, _u64, _u64, _p, _p, _p, _p, _p,
                                           _p, _p, ctypes.c_int]

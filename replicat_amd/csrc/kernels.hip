@@ -50,9 +50,9 @@ constexpr int kStreamAux = RC_DIAG_STREAM_AUX;  // the streamed bytes' cache pol
 // The tile ring reads through a buffer resource based at the tile: the lane offset stays in one
 // VGPR for the whole kernel and the slot offset is an SGPR, so a reissue costs no address VALU
 // (a 64-bit global address would need a v_add_co/v_addc pair per 4 KiB of immediate range).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const uint8_t *base) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(base), 0, 0xffffffffu,
-                                             0x00020000);
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const uint8_t *base,
+                                                             uint32_t bytes = 0xffffffffu) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(base), 0, bytes, 0x00020000);
 }
 __device__ __forceinline__ u32x4 ring_load(__amdgpu_buffer_rsrc_t r, uint32_t lane_off, int it) {
     return __builtin_amdgcn_raw_buffer_load_b128(r, lane_off, it * 1024, kStreamAux);
@@ -270,7 +270,7 @@ struct TileRef {  // 24 bytes, no padding: a padded copy left two 7-byte allocas
     const uint8_t *base;
     uint64_t j0;
     uint32_t s;     // its stream (< 2^31, checked by the host)
-    uint32_t fast;  // 0 / 1
+    uint32_t fast;  // 0: not fast; else the 256-key slices to read (kTileIters; fewer: kClip)
 };
 
 // j0 + 4095 <= jmax, with jmax = (L - 4) / 4 the last key whose 8 bytes exist (adapters.cpp:73)
@@ -338,7 +338,10 @@ __device__ __forceinline__ void tile_scan(const TileRef &tr, const TileRef &nx,
     // no next fast tile (end of the wave's range): harmlessly re-read this tile instead, so
     // the ring loads stay unconditional
     const uint8_t *nbase = nx.fast ? nx.base + 4 * nx.j0 : tr.base + 4 * tr.j0;
-    const __amdgpu_buffer_rsrc_t nsrc = tile_rsrc(nbase);
+    // G > 1: a stream's last tile reads only its slices up to the last needed key (TileCursor
+    // kClip); loads past the resource's range return zeros without touching memory
+    const __amdgpu_buffer_rsrc_t nsrc =
+        G > 1 ? tile_rsrc(nbase, (nx.fast ? nx.fast : tr.fast) * 1024u) : tile_rsrc(nbase);
     uint32_t carry = pf_entry(prev_word, lb_a, lb_b);
     // the word before the next tile; a stream's tile 0 has none (its key 0 is masked below),
     // so it re-reads its own first word rather than the 4 bytes before the stream
@@ -388,7 +391,8 @@ __device__ __forceinline__ void tile_scan(const TileRef &tr, const TileRef &nx,
         const uint32_t b1 = key_top16(e0, e1), b2 = key_top16(e1, e2), b3 = key_top16(e2, e3);
         // the slice's maximum; its index ORed in low: "first" prefers the earliest slice
         // (15 - it), "last" the latest (it)
-        const uint32_t sm = max_u32_op(max3_u32(b0, b1, b2), b3);
+        uint32_t sm = max_u32_op(max3_u32(b0, b1, b2), b3);
+        if constexpr (G > 1) sm &= (uint32_t)it < tr.fast ? ~0u : 0u;  // a clipped slice: no keys
         acc_first = max_u32_op(acc_first, sm | (uint32_t)(kTileIters - 1 - it));
         acc_last = max_u32_op(acc_last, sm | (uint32_t)it);
         if constexpr (G > 1) {
@@ -442,13 +446,18 @@ __device__ __forceinline__ uint32_t wave_max_pk16(uint32_t v) {
 // Walks a wave's tile range across stream boundaries (all state wave-uniform).  kCache: the
 // stream's pointer and fast-tile count are loaded when the cursor enters it, not per tile (scalar
 // loads share lgkmcnt with the LDS reads, so each one in flight is a wait the next LDS use pays
-// for); off for rc_tile_kernel<4>, whose SGPRs would spill.
-template <bool kCache>
+// for); round 6: on for rc_tile_kernel<4> too (its SGPRs fit since the SDWA scan).
+// kClip (round 6, rc_tile_kernel<4>): TileRef.fast of a stream's LAST tile is the number of its
+// 256-key slices up to the stream's last needed key, not 16: the ring reads only those (the
+// buffer resource's range ends there) and the scan masks the rest -- config 3 (iii)'s 1 MiB
+// streams need 2 of their last tile's 16 slices, 1.5 % of the bytes the kernel read before.
+template <bool kCache, bool kClip = false>
 struct TileCursor {
     StreamDesc d;
     uint64_t s, cur, next;
     const uint8_t *base;
     uint32_t nfast;  // the stream's tiles 0 .. nfast - 1 are on the fast path (tile_fast)
+    uint32_t nlast;  // kClip: the slices of the stream's last tile holding needed keys
     __device__ void enter() {
         if constexpr (!kCache) return;
         base = sload_ptr(d.ptr + s);
@@ -456,6 +465,10 @@ struct TileCursor {
         // tile_fast(j0, L) for j0 = i * kTileKeys  <=>  i < nfast
         nfast = L >= 8 && (L - 4) / 4 >= kTileKeys - 1
                     ? (uint32_t)(((L - 4) / 4 - (kTileKeys - 1)) / kTileKeys + 1) : 0u;
+        if constexpr (kClip) {
+            const uint64_t jl = sload(d.jneed + s) - (next - cur - 1) * kTileKeys;
+            nlast = jl < (uint64_t)kTileKeys ? (uint32_t)(jl >> 8) + 1u : (uint32_t)kTileIters;
+        }
     }
     __device__ void init(const StreamDesc &dd, uint64_t n_streams, uint64_t t) {
         d = dd;
@@ -484,7 +497,7 @@ struct TileCursor {
         r.s = (uint32_t)s;
         if constexpr (kCache) {
             r.base = base;
-            r.fast = t - cur < nfast;
+            r.fast = t - cur < nfast ? (kClip && t + 1 == next ? nlast : (uint32_t)kTileIters) : 0u;
         } else {
             r.base = sload_ptr(d.ptr + s);
             r.fast = __builtin_amdgcn_readfirstlane((uint32_t)tile_fast(r.j0, sload(d.len + s))) != 0;
@@ -773,7 +786,7 @@ __global__ __launch_bounds__(1024) void rc_tile_kernel(const KeyTables *__restri
     RC_TILE_STAMP_BEGIN();
 
     // the first fast tile, possibly in a later unit (units without one list no ties)
-    TileCursor<G == 1> cursor;
+    TileCursor<true, (G > 1)> cursor;
     TileRef cur;
     uint64_t t = ub;
     bool seek = true;

@@ -309,8 +309,10 @@ def test_tile_group_maxima_vs_oracle(kind):
         eg = np.zeros(max(nt, 1), np.uint64)
         eh = np.zeros((max(nt, 1), 4), np.uint64)
         buf = np.concatenate([d, np.zeros(16, np.uint8)])
-        o.lib().oc_tile_groups(k0, k1, buf.ctypes.data, n, tk, nt, 4, eg.ctypes.data)
-        o.lib().oc_tile_groups_hot(k0, k1, buf.ctypes.data, n, tk, nt, 4, hot, eh.ctypes.data)
+        # a stream's last tile is read up to the slice holding jneed (round 6, oc_clip_end)
+        o.lib().oc_tile_groups(k0, k1, buf.ctypes.data, n, jneed, tk, nt, 4, eg.ctypes.data)
+        o.lib().oc_tile_groups_hot(k0, k1, buf.ctypes.data, n, jneed, tk, nt, 4, hot,
+                                   eh.ctypes.data)
         g, h = gm[base:base + nt], gh[base:base + nt]
         computed = g != none  # a tile sent to the exact path has no bounds at all
         ok = (((g == eg[:nt]) & (h == eh[:nt]).all(axis=1)) |
