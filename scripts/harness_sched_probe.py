@@ -101,8 +101,18 @@ for r in range(rounds):
             t0 = st[ok].min()
             ends = (en[ok] - t0) / 100.0
             q = np.percentile(ends, [0, 10, 50, 90, 100])
+            starts = (st[ok] - t0) / 100.0
+            # round 6: per workgroup (16 waves), when its first and last wave ended
+            wg = np.arange(len(en))[ok] // 16
+            wg_first = np.array([ends[wg == g].min() for g in np.unique(wg)])
+            wg_last = np.array([ends[wg == g].max() for g in np.unique(wg)])
             res[s]['stamps'].append({'end_us_0_10_50_90_100': [round(float(x), 1) for x in q],
                                      'mean_end_us': round(float(ends.mean()), 1),
+                                     'start_us_0_50_100': [round(float(x), 1) for x in
+                                                           np.percentile(starts, [0, 50, 100])],
+                                     'wg_last_end_us_0_50_100': [round(float(x), 1) for x in
+                                                                 np.percentile(wg_last, [0, 50, 100])],
+                                     'wg_spread_us_median': round(float(np.median(wg_last - wg_first)), 1),
                                      'tiles_min_max': [int(kk[ok].min()), int(kk[ok].max())]})
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ch.read_probe(pool.data_ptr(), nbytes, out.data_ptr(), hs)
