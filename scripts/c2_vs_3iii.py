@@ -5,7 +5,10 @@ MiB, replicat's defaults, pipelined steps as bench.py runs them) and as config 3
 sequence), K back-to-back steps each, rounds in ABBA order; median wall ms per step, the tile
 kernel's HIP-event time and the bytes each reads.
 
-    python scripts/c2_vs_3iii.py [rounds] [steps]
+    python scripts/c2_vs_3iii.py [rounds] [steps] [--piped]
+
+--piped (round 6): also config 3 (iii) on a chunker created with RC_PIPE_ALL=1, so that its
+steps overlap as config 2's do -- the three setups on the same allocation.
 """
 import json
 import os
@@ -20,17 +23,25 @@ import torch  # noqa: E402
 from replicat_amd import synth  # noqa: E402
 from replicat_amd.chunker import GpuChunker, fill_splitmix_streams, keys_needed  # noqa: E402
 
-rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 4
-K = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+argv = [a for a in sys.argv[1:] if not a.startswith('--')]
+rounds = int(argv[0]) if len(argv) > 0 else 4
+K = int(argv[1]) if len(argv) > 1 else 10
+PIPED = '--piped' in sys.argv
 torch.cuda.set_stream(torch.cuda.Stream())
 hs = torch.cuda.current_stream().cuda_stream
 GIB = 1 << 30
 pool = torch.empty((64 << 30) + 64, dtype=torch.uint8, device='cuda')
 fill_splitmix_streams(pool.data_ptr(), 1024, 64 << 20, 64 << 20, synth.DEFAULT_SEED, 0, 1, hs)
 setups = {}
-for name, n, size, mn, mx in (('config2', 1024, 64 << 20, 128_000, 5_120_000),
-                              ('config3iii', 65536, 1 << 20, 2_000, 80_000)):
+cases = [('config2', 1024, 64 << 20, 128_000, 5_120_000),
+         ('config3iii', 65536, 1 << 20, 2_000, 80_000)]
+if PIPED:
+    cases.append(('config3iii_piped', 65536, 1 << 20, 2_000, 80_000))
+for name, n, size, mn, mx in cases:
+    if name.endswith('_piped'):  # knobs are read when the chunker is created
+        os.environ['RC_PIPE_ALL'] = '1'
     ch = GpuChunker(mn, mx, b'\xff' * 16)
+    os.environ.pop('RC_PIPE_ALL', None)
     total, caps = ch.capacity([size] * n)
     j = keys_needed(mx, size, 0)
     setups[name] = dict(
@@ -71,4 +82,7 @@ for name, v in res.items():
                  'GiBps': round((64 << 30) / (med[0] * 1e-3) / GIB, 1),
                  'bytes_read': setups[name]['read'], 'pipelined_calls': int(a[-1, 2])}
 out['3iii_over_config2'] = round(out['config3iii']['ms_per_step'] / out['config2']['ms_per_step'], 4)
+if PIPED:
+    out['3iii_piped_over_config2'] = round(out['config3iii_piped']['ms_per_step'] /
+                                           out['config2']['ms_per_step'], 4)
 print(json.dumps(out), flush=True)
