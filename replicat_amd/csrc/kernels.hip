@@ -344,9 +344,16 @@ __device__ __forceinline__ void tile_scan(const TileRef &tr, const TileRef &nx,
         G > 1 ? tile_rsrc(nbase, (nx.fast ? nx.fast : tr.fast) * 1024u) : tile_rsrc(nbase);
     uint32_t carry = pf_entry(prev_word, lb_a, lb_b);
     // the word before the next tile; a stream's tile 0 has none (its key 0 is masked below),
-    // so it re-reads its own first word rather than the 4 bytes before the stream
+    // so it re-reads its own first word rather than the 4 bytes before the stream.  Round 6: a
+    // next tile that follows this one in its stream takes it from the ring instead (this tile's
+    // last word: lane 63 of slice 15), and the load reads nothing -- a buffer resource of range 0
+    // keeps it one vector-memory instruction, so every tile issues the same sequence (a third of
+    // the kernel's auxiliary requests: those cost the scan ~1 %, profiles/r06/aux_loads/)
     const uint64_t nj0 = nx.fast ? nx.j0 : tr.j0;
-    prev_word = ld_u32(nj0 ? nbase - 4 : nbase);
+    const bool consec = nx.fast && nx.s == tr.s && nx.j0 == tr.j0 + kTileKeys;
+    const uint32_t pw_loaded = __builtin_amdgcn_raw_buffer_load_b32(
+        tile_rsrc(nj0 ? nbase - 4 : nbase, consec ? 0u : 4u), 0, 0, 0);
+    uint32_t last_w = 0;
     // key 0 of a stream (local index 0 of lane 0 in tile 0) does not exist: i starts at 4
     // (adapters.cpp:59).  Its top-16 value is zeroed, so it never raises a slice maximum.
     const uint32_t key0_mask = (tr.j0 == 0 && lane == 0) ? 0u : ~0u;
@@ -360,6 +367,7 @@ __device__ __forceinline__ void tile_scan(const TileRef &tr, const TileRef &nx,
         pf_addrs(x[it].y, lb_a, lb_b, a + 4);
         pf_addrs(x[it].z, lb_a, lb_b, a + 8);
         pf_addrs(x[it].w, lb_a, lb_b, a + 12);
+        if (it == kTileIters - 1) last_w = (uint32_t)__builtin_amdgcn_readlane(x[it].w, 63);
         x[it] = ring_load(nsrc, lane * 16, it);
         // the slice's 16 lookups issued together, then folded (round 5): left to itself the
         // scheduler gave every variant but rc_tile_kernel<1, false> a low-pressure order -- 3-4
@@ -408,6 +416,7 @@ __device__ __forceinline__ void tile_scan(const TileRef &tr, const TileRef &nx,
     top = acc_first >> 16;
     fs = (uint32_t)(kTileIters - 1) - (acc_first & 0xffffu);
     ls = acc_last & 0xffffu;
+    prev_word = consec ? last_w : pw_loaded;
 }
 
 // Maximum over the wave, returned in SGPRs: DPP shifts within each 16-lane row, then the
